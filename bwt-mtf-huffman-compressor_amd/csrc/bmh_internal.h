@@ -1,0 +1,125 @@
+// bmh_internal.h — shared internals of libbmh: the per-GPU context (stream, workspace arena,
+// per-kernel HIP-event timing) and error plumbing. Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/bmh.h"
+
+namespace bmh {
+
+struct Error : std::runtime_error {
+    bmh_status status;
+    Error(bmh_status s, const std::string &m) : std::runtime_error(m), status(s) {}
+};
+
+[[noreturn]] void fail(bmh_status s, const std::string &msg);
+void set_last_error(const std::string &msg);
+
+#define BMH_HIP(call)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (call);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            ::bmh::fail(BMH_EHIP, std::string(#call) + ": " + hipGetErrorString(e_) + " @" + \
+                                      __FILE__ + ":" + std::to_string(__LINE__));              \
+    } while (0)
+
+struct KStat {
+    uint64_t launches = 0;
+    double ms = 0.0;
+};
+
+// Grow-only device buffers keyed by slot; reused across calls so the hot path does no
+// hipMalloc (arrays are sized for the largest batch seen).
+enum Slot : int {
+    WS_SA, WS_SA2, WS_RKA, WS_RKB, WS_KEY, WS_KEY2, WS_SEG_CUR, WS_SEG_NXT, WS_TINY, WS_MED,
+    WS_LARGE, WS_LARGE2, WS_GROUPS, WS_PREFIX, WS_SCAN_PART, WS_TILES, WS_BLOCKS, WS_OFFS,
+    WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_L, WS_MTF,
+    WS_MTF_R, WS_MTF_S, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
+    WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_RESOLVED, WS_COUNT_
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    std::map<std::string, KStat> stats;
+    struct Pending {
+        const char *name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    void *ws[WS_COUNT_] = {};
+    size_t ws_size[WS_COUNT_] = {};
+    // pinned host staging
+    void *pinned = nullptr;
+    size_t pinned_size = 0;
+
+    void *get(Slot s, size_t bytes);
+    void *host_pinned(size_t bytes);
+    void sync();  // stream sync + resolve timing events
+    hipEvent_t ev();
+    int tbegin(const char *name);  // -1 when timing is off
+    void tend(int idx);
+};
+
+// Kernel launch on the context stream, bracketed by timing events when enabled.
+#define BMH_LAUNCH(ctx, kname, kern, grid, block, shmem, ...)                             \
+    do {                                                                                  \
+        const int p_ = (ctx)->tbegin(kname);                                              \
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(block), shmem, (ctx)->stream, __VA_ARGS__); \
+        BMH_HIP(hipGetLastError());                                                       \
+        (ctx)->tend(p_);                                                                  \
+    } while (0)
+
+// Batch description shared by the stages.
+struct BlockInfo {
+    uint32_t off;     // global byte offset of the block in the batch buffer
+    uint32_t n;       // block length
+};
+
+struct Batch {
+    std::vector<uint64_t> offs;  // nblocks + 1
+    uint32_t nblocks = 0;
+    uint64_t total = 0;
+    uint32_t max_n = 0;
+};
+Batch make_batch(const uint64_t *offs, uint32_t nblocks);
+
+// Stage implementations (device buffers, host-synchronous).
+void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
+void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,
+               uint32_t *h_first32);
+void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
+                const uint64_t *pay_offs);
+void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);
+void write_headers(Ctx *c, uint8_t *d_out, const std::vector<uint8_t> &hdr_bytes,
+                   const std::vector<uint64_t> &hdr_src_offs, const std::vector<uint64_t> &rec_offs);
+void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
+
+// Host Huffman (huffman_host.cpp)
+void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out);
+uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);
+
+// Records / container / decode (record.cpp)
+constexpr uint64_t kRecordHeader = 24;
+void put_u64(uint8_t *p, uint64_t v);
+uint64_t get_u64(const uint8_t *p);
+extern const uint8_t kContainerMagic[8];
+uint64_t record_n(const uint8_t *rec, uint64_t len);
+void record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out);
+void decode_record(const uint8_t *rec, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
+bool is_container(const uint8_t *in, uint64_t len);
+void decompress(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
+
+}  // namespace bmh
+
+struct bmh_ctx : bmh::Ctx {};

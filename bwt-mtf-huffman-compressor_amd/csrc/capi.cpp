@@ -1,0 +1,631 @@
+// capi.cpp — the C ABI (include/bmh.h): contexts, workspace, timing, and the batch encode
+// that chains the three device stages with the host Huffman build in between.
+//
+// Orchestration of one batch (compress(), reference main.cpp:300-325, minus file I/O):
+//   bwt kernels -> L, primary        (bwt(), main.cpp:77-91)
+//   mtf kernels -> MTF, freq, first  (move_to_front() main.cpp:93-112, huffman() :231-244)
+//   host        -> code tables, tree bytes, record sizes/offsets (huffman() :245-254, :132-196)
+//   pack kernels-> payloads in place behind the headers (encode_with_huffman() :158-172,
+//                  write_bytes() io_utilities.h:7-27)
+#include "bmh_internal.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <thread>
+
+namespace bmh {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+[[noreturn]] void fail(bmh_status s, const std::string &msg) { throw Error(s, msg); }
+
+void *Ctx::get(Slot s, size_t bytes)
+{
+    if (bytes == 0) bytes = 1;
+    if (ws_size[s] >= bytes) return ws[s];
+    if (ws[s]) {
+        BMH_HIP(hipStreamSynchronize(stream));
+        BMH_HIP(hipFree(ws[s]));
+        ws[s] = nullptr;
+        ws_size[s] = 0;
+    }
+    size_t sz = ((bytes + bytes / 8) + 255) & ~(size_t)255;
+    void *p = nullptr;
+    if (hipMalloc(&p, sz) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(BMH_ENOMEM, "device allocation of " + std::to_string(sz) + " bytes failed");
+    }
+    ws[s] = p;
+    ws_size[s] = sz;
+    return p;
+}
+
+void *Ctx::host_pinned(size_t bytes)
+{
+    if (pinned_size >= bytes) return pinned;
+    if (pinned) {
+        BMH_HIP(hipStreamSynchronize(stream));
+        BMH_HIP(hipHostFree(pinned));
+        pinned = nullptr;
+    }
+    size_t sz = std::max<size_t>(bytes, 1 << 16);
+    BMH_HIP(hipHostMalloc(&pinned, sz, hipHostMallocDefault));
+    pinned_size = sz;
+    return pinned;
+}
+
+hipEvent_t Ctx::ev()
+{
+    if (!event_pool.empty()) {
+        hipEvent_t e = event_pool.back();
+        event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    BMH_HIP(hipEventCreate(&e));
+    return e;
+}
+
+int Ctx::tbegin(const char *name)
+{
+    if (!timing) return -1;
+    Pending p{name, ev(), ev()};
+    BMH_HIP(hipEventRecord(p.a, stream));
+    pending.push_back(p);
+    return (int)pending.size() - 1;
+}
+
+void Ctx::tend(int idx)
+{
+    if (idx < 0) return;
+    BMH_HIP(hipEventRecord(pending[idx].b, stream));
+}
+
+void Ctx::sync()
+{
+    BMH_HIP(hipStreamSynchronize(stream));
+    for (auto &p : pending) {
+        float ms = 0.f;
+        BMH_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        KStat &k = stats[p.name];
+        k.launches++;
+        k.ms += ms;
+        event_pool.push_back(p.a);
+        event_pool.push_back(p.b);
+    }
+    pending.clear();
+}
+
+Batch make_batch(const uint64_t *offs, uint32_t nblocks)
+{
+    if (!offs || nblocks == 0) fail(BMH_EINVAL, "batch: no blocks");
+    Batch b;
+    b.nblocks = nblocks;
+    b.offs.assign(offs, offs + nblocks + 1);
+    for (uint32_t i = 0; i < nblocks; ++i) {
+        if (offs[i + 1] <= offs[i])
+            fail(BMH_EINVAL, "batch: empty or negative block " + std::to_string(i) +
+                                 " (the reference segfaults on empty input)");
+        const uint64_t n = offs[i + 1] - offs[i];
+        if (n >= 0xffffffffull) fail(BMH_ERANGE, "batch: block larger than 4 GiB - 2");
+        b.max_n = std::max<uint32_t>(b.max_n, (uint32_t)n);
+    }
+    b.total = offs[nblocks] - offs[0];
+    if (offs[0] != 0) fail(BMH_EINVAL, "batch: offs[0] must be 0");
+    if (b.total >= 0xffffffffull) fail(BMH_ERANGE, "batch: total must be < 4 GiB");
+    if (nblocks > 65535) fail(BMH_ERANGE, "batch: at most 65535 blocks per call");
+    return b;
+}
+
+uint64_t record_bound(uint64_t n) { return kRecordHeader + 320 + n + 16; }
+
+// Device batch encode -> records at d_out; fills rec_offs (nblocks + 1).
+void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
+                   uint64_t *rec_offs)
+{
+    const uint32_t nb = bt.nblocks;
+    uint8_t *d_L = (uint8_t *)c->get(WS_L, bt.total);
+    uint8_t *d_mtf = (uint8_t *)c->get(WS_MTF, bt.total);
+    std::vector<uint64_t> prim(nb);
+    bwt_batch(c, d_in, bt, d_L, prim.data());
+    std::vector<uint32_t> f32((size_t)nb * 256), fi32((size_t)nb * 256);
+    mtf_batch(c, d_L, bt, d_mtf, f32.data(), fi32.data());
+
+    std::vector<bmh_code_table> tabs(nb);
+    std::vector<uint64_t> pay(nb);
+    auto build = [&](uint32_t b0, uint32_t b1) {
+        for (uint32_t b = b0; b < b1; ++b) {
+            uint64_t freq[256], first[256];
+            for (int s = 0; s < 256; ++s) {
+                freq[s] = f32[(size_t)b * 256 + s];
+                const uint32_t f = fi32[(size_t)b * 256 + s];
+                first[s] = f == 0xffffffffu ? UINT64_MAX : f;
+            }
+            huffman_build(freq, first, &tabs[b]);
+            pay[b] = payload_bytes(&tabs[b], freq);
+        }
+    };
+    if (nb >= 64) {  // trees are independent: spread over a few host threads
+        const uint32_t nt = std::min<uint32_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> th;
+        std::vector<std::string> err(nt);
+        for (uint32_t t = 0; t < nt; ++t)
+            th.emplace_back([&, t]() {
+                try {
+                    build(nb * t / nt, nb * (t + 1) / nt);
+                } catch (const std::exception &e) {
+                    err[t] = e.what();
+                }
+            });
+        for (auto &x : th) x.join();
+        for (auto &e : err)
+            if (!e.empty()) fail(BMH_ERANGE, e);
+    } else {
+        build(0, nb);
+    }
+    rec_offs[0] = 0;
+    std::vector<uint64_t> src(nb + 1, 0), roffs(nb + 1, 0), pay_offs(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t hl = kRecordHeader + tabs[b].tree_len;
+        src[b + 1] = src[b] + hl;
+        roffs[b + 1] = roffs[b] + hl + pay[b];
+        pay_offs[b] = roffs[b] + hl;
+    }
+    if (roffs[nb] > out_cap) fail(BMH_ERANGE, "encode: output capacity too small");
+    std::vector<uint8_t> hdr(src[nb]);
+    for (uint32_t b = 0; b < nb; ++b) {
+        uint8_t *h = &hdr[src[b]];
+        put_u64(h, prim[b]);
+        put_u64(h + 8, bt.offs[b + 1] - bt.offs[b]);
+        put_u64(h + 16, tabs[b].tree_len);
+        memcpy(h + 24, tabs[b].tree, tabs[b].tree_len);
+    }
+    BMH_HIP(hipMemsetAsync(d_out, 0, roffs[nb], c->stream));
+    write_headers(c, d_out, hdr, src, roffs);
+    pack_batch(c, d_mtf, bt, tabs.data(), d_out, pay_offs.data());
+    for (uint32_t b = 0; b <= nb; ++b) rec_offs[b] = roffs[b];
+}
+
+static uint64_t max_batch_bytes()
+{
+    const char *e = getenv("BMH_MAX_BATCH");
+    uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return v ? v : (1ull << 30);
+}
+
+// Encode host blocks [b0, b1) of `in` (block size bs); appends records to recs/lens.
+static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t bs, const std::vector<uint64_t> &blist,
+                               std::vector<std::vector<uint8_t>> &recs)
+{
+    const uint64_t cap_batch = max_batch_bytes();
+    size_t i = 0;
+    while (i < blist.size()) {
+        // gather consecutive (in blist order) blocks up to the batch cap
+        std::vector<uint64_t> offs{0};
+        size_t j = i;
+        while (j < blist.size()) {
+            const uint64_t b = blist[j];
+            const uint64_t len = std::min(bs, n - b * bs);
+            if (j > i && offs.back() + len > cap_batch) break;
+            offs.push_back(offs.back() + len);
+            ++j;
+        }
+        const uint32_t nbk = (uint32_t)(j - i);
+        Batch bt = make_batch(offs.data(), nbk);
+        uint8_t *d_in = (uint8_t *)c->get(WS_IN, bt.total);
+        for (size_t k = i; k < j; ++k) {
+            const uint64_t b = blist[k];
+            BMH_HIP(hipMemcpyAsync(d_in + offs[k - i], in + b * bs, offs[k - i + 1] - offs[k - i],
+                                   hipMemcpyHostToDevice, c->stream));
+        }
+        uint64_t cap = 0;
+        for (uint32_t k = 0; k < nbk; ++k) cap += record_bound(offs[k + 1] - offs[k]);
+        uint8_t *d_out = (uint8_t *)c->get(WS_OUT, cap);
+        std::vector<uint64_t> ro(nbk + 1);
+        encode_blocks(c, d_in, bt, d_out, cap, ro.data());
+        for (uint32_t k = 0; k < nbk; ++k) {
+            std::vector<uint8_t> r(ro[k + 1] - ro[k]);
+            BMH_HIP(hipMemcpyAsync(r.data(), d_out + ro[k], r.size(), hipMemcpyDeviceToHost, c->stream));
+            recs.push_back(std::move(r));
+        }
+        c->sync();
+        i = j;
+    }
+}
+
+static void assemble(uint64_t n, uint64_t bs, uint64_t nblocks, std::vector<std::vector<uint8_t>> &recs, uint8_t *out,
+                     uint64_t out_cap, uint64_t *out_len)
+{
+    uint64_t total = 0;
+    if (nblocks == 1) {
+        total = recs[0].size();
+        if (total > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
+        memcpy(out, recs[0].data(), total);
+    } else {
+        total = 32 + 8 * nblocks;
+        for (auto &r : recs) total += r.size();
+        if (total > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
+        memcpy(out, kContainerMagic, 8);
+        put_u64(out + 8, bs);
+        put_u64(out + 16, nblocks);
+        put_u64(out + 24, n);
+        uint64_t o = 32 + 8 * nblocks;
+        for (uint64_t b = 0; b < nblocks; ++b) {
+            put_u64(out + 32 + 8 * b, recs[b].size());
+            memcpy(out + o, recs[b].data(), recs[b].size());
+            o += recs[b].size();
+        }
+    }
+    *out_len = total;
+}
+
+}  // namespace bmh
+
+using namespace bmh;
+
+#define API_BEGIN try {
+#define API_END                                      \
+    }                                                \
+    catch (const Error &e)                           \
+    {                                                \
+        set_last_error(e.what());                    \
+        return e.status;                             \
+    }                                                \
+    catch (const std::bad_alloc &)                   \
+    {                                                \
+        set_last_error("host allocation failed");    \
+        return BMH_ENOMEM;                           \
+    }                                                \
+    catch (const std::exception &e)                  \
+    {                                                \
+        set_last_error(e.what());                    \
+        return BMH_EINVAL;                           \
+    }                                                \
+    set_last_error("");                              \
+    return BMH_OK;
+
+static void use_device(bmh_ctx *c)
+{
+    if (!c) fail(BMH_EINVAL, "null context");
+    BMH_HIP(hipSetDevice(c->device));
+}
+
+extern "C" {
+
+const char *bmh_version(void) { return "bmh 0.1.0 (gfx950)"; }
+
+const char *bmh_status_str(int s)
+{
+    switch (s) {
+    case BMH_OK: return "ok";
+    case BMH_EINVAL: return "invalid argument";
+    case BMH_ENOMEM: return "out of memory";
+    case BMH_EHIP: return "HIP runtime error";
+    case BMH_ERANGE: return "size limit exceeded";
+    case BMH_ECORRUPT: return "corrupt input";
+    case BMH_ENODEV: return "no gfx950 device";
+    default: return "unknown status";
+    }
+}
+
+const char *bmh_last_error(void) { return g_last_error.c_str(); }
+
+int bmh_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+bmh_status bmh_ctx_create(int device, bmh_ctx **out)
+{
+    API_BEGIN
+    if (!out) fail(BMH_EINVAL, "null out pointer");
+    *out = nullptr;
+    const int n = bmh_device_count();
+    if (device < 0 || device >= n) fail(BMH_ENODEV, "no HIP device " + std::to_string(device));
+    hipDeviceProp_t prop;
+    BMH_HIP(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        fail(BMH_ENODEV, std::string("device is ") + prop.gcnArchName + ", libbmh is built for gfx950");
+    BMH_HIP(hipSetDevice(device));
+    bmh_ctx *c = new bmh_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        fail(BMH_EHIP, "stream creation failed");
+    }
+    *out = c;
+    API_END
+}
+
+void bmh_ctx_destroy(bmh_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (int s = 0; s < WS_COUNT_; ++s)
+        if (c->ws[s]) (void)hipFree(c->ws[s]);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    for (auto &p : c->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+void *bmh_ctx_stream(bmh_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+bmh_status bmh_dev_alloc(bmh_ctx *c, uint64_t bytes, void **d_ptr)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_ptr) fail(BMH_EINVAL, "null out pointer");
+    if (hipMalloc(d_ptr, bytes ? bytes : 1) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(BMH_ENOMEM, "hipMalloc failed");
+    }
+    API_END
+}
+
+bmh_status bmh_dev_free(bmh_ctx *c, void *d_ptr)
+{
+    API_BEGIN
+    use_device(c);
+    BMH_HIP(hipStreamSynchronize(c->stream));
+    BMH_HIP(hipFree(d_ptr));
+    API_END
+}
+
+bmh_status bmh_memcpy_h2d(bmh_ctx *c, void *d_dst, const void *h_src, uint64_t bytes)
+{
+    API_BEGIN
+    use_device(c);
+    BMH_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, c->stream));
+    c->sync();
+    API_END
+}
+
+bmh_status bmh_memcpy_d2h(bmh_ctx *c, void *h_dst, const void *d_src, uint64_t bytes)
+{
+    API_BEGIN
+    use_device(c);
+    BMH_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+    API_END
+}
+
+bmh_status bmh_bwt_dev(bmh_ctx *c, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks, uint8_t *d_L,
+                       uint64_t *h_primary)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_in || !d_L || !h_primary) fail(BMH_EINVAL, "null buffer");
+    Batch bt = make_batch(offs, nblocks);
+    bwt_batch(c, d_in, bt, d_L, h_primary);
+    API_END
+}
+
+bmh_status bmh_mtf_dev(bmh_ctx *c, const uint8_t *d_L, const uint64_t *offs, uint32_t nblocks, uint8_t *d_mtf,
+                       uint64_t *h_freq, uint64_t *h_first)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_L || !d_mtf) fail(BMH_EINVAL, "null buffer");
+    Batch bt = make_batch(offs, nblocks);
+    std::vector<uint32_t> f((size_t)nblocks * 256), fi((size_t)nblocks * 256);
+    mtf_batch(c, d_L, bt, d_mtf, f.data(), fi.data());
+    for (size_t i = 0; i < f.size(); ++i) {
+        if (h_freq) h_freq[i] = f[i];
+        if (h_first) h_first[i] = fi[i] == 0xffffffffu ? UINT64_MAX : fi[i];
+    }
+    API_END
+}
+
+bmh_status bmh_histogram_dev(bmh_ctx *c, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks, uint64_t *h_freq,
+                             uint64_t *h_first)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_in || !h_freq) fail(BMH_EINVAL, "null argument");
+    Batch bt = make_batch(offs, nblocks);
+    std::vector<uint32_t> f((size_t)nblocks * 256), fi((size_t)nblocks * 256);
+    histogram_batch(c, d_in, bt, f.data(), fi.data());
+    for (size_t i = 0; i < f.size(); ++i) {
+        h_freq[i] = f[i];
+        if (h_first) h_first[i] = fi[i] == 0xffffffffu ? UINT64_MAX : fi[i];
+    }
+    API_END
+}
+
+bmh_status bmh_huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out)
+{
+    API_BEGIN
+    if (!freq || !first || !out) fail(BMH_EINVAL, "null argument");
+    huffman_build(freq, first, out);
+    API_END
+}
+
+uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
+{
+    return (t && freq) ? payload_bytes(t, freq) : 0;
+}
+
+bmh_status bmh_pack_dev(bmh_ctx *c, const uint8_t *d_mtf, const uint64_t *offs, uint32_t nblocks,
+                        const bmh_code_table *tables, uint8_t *d_out, const uint64_t *pay_offs)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_mtf || !tables || !d_out || !pay_offs) fail(BMH_EINVAL, "null argument");
+    Batch bt = make_batch(offs, nblocks);
+    pack_batch(c, d_mtf, bt, tables, d_out, pay_offs);
+    API_END
+}
+
+bmh_status bmh_encode_blocks_dev(bmh_ctx *c, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
+                                 uint8_t *d_out, uint64_t out_cap, uint64_t *h_rec_offs)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_in || !d_out || !h_rec_offs) fail(BMH_EINVAL, "null argument");
+    Batch bt = make_batch(offs, nblocks);
+    encode_blocks(c, d_in, bt, d_out, out_cap, h_rec_offs);
+    API_END
+}
+
+uint64_t bmh_record_bound(uint64_t n) { return record_bound(n); }
+
+uint64_t bmh_compress_bound(uint64_t n, uint64_t bs)
+{
+    if (bs == 0 || bs >= n) return record_bound(n);
+    const uint64_t nb = (n + bs - 1) / bs;
+    return 32 + 8 * nb + nb * (kRecordHeader + 320 + 16) + n;
+}
+
+bmh_status bmh_compress_host(bmh_ctx *c, const uint8_t *in, uint64_t n, uint64_t block_size, uint8_t *out,
+                             uint64_t out_cap, uint64_t *out_len)
+{
+    bmh_ctx *cs[1] = {c};
+    return bmh_compress_host_multi(cs, 1, in, n, block_size, out, out_cap, out_len);
+}
+
+bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t *in, uint64_t n, uint64_t block_size,
+                                   uint8_t *out, uint64_t out_cap, uint64_t *out_len)
+{
+    API_BEGIN
+    if (!ctxs || nctx == 0 || !in || !out || !out_len) fail(BMH_EINVAL, "null argument");
+    if (n == 0) fail(BMH_EINVAL, "empty input (the reference segfaults on empty input)");
+    const uint64_t bs = (block_size == 0 || block_size >= n) ? n : block_size;
+    if (bs >= 0xffffffffull) fail(BMH_ERANGE, "block size must be < 4 GiB - 1");
+    const uint64_t nblocks = (n + bs - 1) / bs;
+    std::vector<std::vector<uint8_t>> recs(nblocks);
+    std::vector<std::string> err(nctx);
+    std::vector<bmh_status> st(nctx, BMH_OK);
+    auto work = [&](uint32_t g) {
+        try {
+            use_device(ctxs[g]);
+            std::vector<uint64_t> bl;
+            for (uint64_t b = g; b < nblocks; b += nctx) bl.push_back(b);
+            std::vector<std::vector<uint8_t>> mine;
+            encode_host_blocks(ctxs[g], in, n, bs, bl, mine);
+            for (size_t k = 0; k < bl.size(); ++k) recs[bl[k]] = std::move(mine[k]);
+        } catch (const Error &e) {
+            st[g] = e.status;
+            err[g] = e.what();
+        } catch (const std::exception &e) {
+            st[g] = BMH_EINVAL;
+            err[g] = e.what();
+        }
+    };
+    if (nctx == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < nctx; ++g) th.emplace_back(work, g);
+        for (auto &t : th) t.join();
+    }
+    for (uint32_t g = 0; g < nctx; ++g)
+        if (st[g] != BMH_OK) fail(st[g], err[g]);
+    assemble(n, bs, nblocks, recs, out, out_cap, out_len);
+    API_END
+}
+
+bmh_status bmh_decompress_host(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out)
+{
+    API_BEGIN
+    if (!in || !n_out) fail(BMH_EINVAL, "null argument");
+    decompress(in, len, out, cap, n_out);
+    API_END
+}
+
+bmh_status bmh_record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out)
+{
+    API_BEGIN
+    if (!rec || !n_out) fail(BMH_EINVAL, "null argument");
+    record_to_mtf(rec, len, mtf, cap, n_out);
+    API_END
+}
+
+int bmh_is_container(const uint8_t *in, uint64_t len) { return in && is_container(in, len) ? 1 : 0; }
+
+bmh_status bmh_container_info(const uint8_t *in, uint64_t len, uint64_t *nblocks, uint64_t *total_n)
+{
+    API_BEGIN
+    if (!in || !is_container(in, len) || len < 32) fail(BMH_ECORRUPT, "not a BMH container");
+    if (nblocks) *nblocks = get_u64(in + 16);
+    if (total_n) *total_n = get_u64(in + 24);
+    API_END
+}
+
+bmh_status bmh_container_record(const uint8_t *in, uint64_t len, uint64_t b, const uint8_t **rec, uint64_t *rec_len)
+{
+    API_BEGIN
+    if (!in || !is_container(in, len) || len < 32) fail(BMH_ECORRUPT, "not a BMH container");
+    const uint64_t nb = get_u64(in + 16);
+    if (b >= nb || nb > (len - 32) / 8) fail(BMH_EINVAL, "block index out of range");
+    uint64_t o = 32 + 8 * nb;
+    for (uint64_t k = 0; k < b; ++k) o += get_u64(in + 32 + 8 * k);
+    const uint64_t l = get_u64(in + 32 + 8 * b);
+    if (o > len || l > len - o) fail(BMH_ECORRUPT, "container: record overruns input");
+    if (rec) *rec = in + o;
+    if (rec_len) *rec_len = l;
+    API_END
+}
+
+bmh_status bmh_ctx_set_timing(bmh_ctx *c, int enable)
+{
+    API_BEGIN
+    use_device(c);
+    c->sync();
+    c->timing = enable != 0;
+    API_END
+}
+
+bmh_status bmh_ctx_reset_stats(bmh_ctx *c)
+{
+    API_BEGIN
+    use_device(c);
+    c->sync();
+    c->stats.clear();
+    API_END
+}
+
+int bmh_ctx_kernel_stats(bmh_ctx *c, char (*names)[64], uint64_t *launches, double *total_ms, int cap)
+{
+    if (!c) return 0;
+    try {
+        c->sync();
+    } catch (...) {
+        return 0;
+    }
+    int i = 0;
+    for (auto &kv : c->stats) {
+        if (i < cap) {
+            if (names) {
+                strncpy(names[i], kv.first.c_str(), 63);
+                names[i][63] = 0;
+            }
+            if (launches) launches[i] = kv.second.launches;
+            if (total_ms) total_ms[i] = kv.second.ms;
+        }
+        ++i;
+    }
+    return i;
+}
+
+bmh_status bmh_synth_splitmix64_dev(bmh_ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_out) fail(BMH_EINVAL, "null buffer");
+    if (nbytes) synth_splitmix64(c, d_out, nbytes, seed, offset);
+    API_END
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+// device_util.h — wave64 / workgroup primitives shared by the kernels (gfx950: wave = 64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace bmh {
+
+constexpr int kWave = 64;
+
+// v_writelane_b32: the LLVM intrinsic bound directly (no clang builtin for it in ROCm 7.2).
+extern "C" __device__ int __bmh_llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t writelane(uint32_t val, uint32_t lane, uint32_t old)
+{
+    return (uint32_t)__bmh_llvm_writelane((int)val, (int)lane, (int)old);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Inclusive wave64 scans.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint64_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x = x > y ? x : y;
+    }
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_incl_min_rev(uint32_t x)  // suffix min (from the right)
+{
+    const uint32_t l = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_down(x, o, 64);
+        if (l + o < 64u) x = x < y ? x : y;
+    }
+    return x;
+}
+
+// Workgroup exclusive sum of one value per thread. s_tmp needs NT/64 + 1 words.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_tmp, uint32_t *total)
+{
+    constexpr int NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6, l = lane_id();
+    uint32_t inc = wave_incl_sum(v);
+    if (l == 63) s_tmp[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        uint32_t t = l < (uint32_t)NW ? s_tmp[l] : 0u;
+        uint32_t ti = wave_incl_sum(t);
+        if (l < (uint32_t)NW) s_tmp[l] = ti - t;
+        if (l == (uint32_t)NW - 1) s_tmp[NW] = ti;
+    }
+    __syncthreads();
+    uint32_t r = s_tmp[w] + inc - v;
+    if (total) *total = s_tmp[NW];
+    __syncthreads();
+    return r;
+}
+
+template <int NT>
+__device__ __forceinline__ uint64_t block_excl_sum64(uint64_t v, uint64_t *s_tmp, uint64_t *total)
+{
+    constexpr int NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6, l = lane_id();
+    uint64_t inc = wave_incl_sum64(v);
+    if (l == 63) s_tmp[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        uint64_t t = l < (uint32_t)NW ? s_tmp[l] : 0ull;
+        uint64_t ti = wave_incl_sum64(t);
+        if (l < (uint32_t)NW) s_tmp[l] = ti - t;
+        if (l == (uint32_t)NW - 1) s_tmp[NW] = ti;
+    }
+    __syncthreads();
+    uint64_t r = s_tmp[w] + inc - v;
+    if (total) *total = s_tmp[NW];
+    __syncthreads();
+    return r;
+}
+
+// Workgroup exclusive max (identity 0) and exclusive suffix min (identity `ident`).
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_max(uint32_t v, uint32_t *s_tmp)
+{
+    constexpr int NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6, l = lane_id();
+    uint32_t inc = wave_incl_max(v);
+    uint32_t prev = __shfl_up(inc, 1, 64);
+    if (l == 0) prev = 0;
+    if (l == 63) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t i = 0; i < w; ++i) carry = carry > s_tmp[i] ? carry : s_tmp[i];
+    __syncthreads();
+    (void)NW;
+    return carry > prev ? carry : prev;
+}
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_min_rev(uint32_t v, uint32_t ident, uint32_t *s_tmp)
+{
+    constexpr int NW = NT / 64;
+    const uint32_t w = threadIdx.x >> 6, l = lane_id();
+    uint32_t inc = wave_incl_min_rev(v);
+    uint32_t nxt = __shfl_down(inc, 1, 64);
+    if (l == 63) nxt = ident;
+    if (l == 0) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t carry = ident;
+    for (uint32_t i = w + 1; i < (uint32_t)NW; ++i) carry = carry < s_tmp[i] ? carry : s_tmp[i];
+    __syncthreads();
+    return carry < nxt ? carry : nxt;
+}
+
+// Block containing global slot g: boffs has nb+1 ascending entries.
+__device__ __forceinline__ uint32_t find_block(const uint32_t *__restrict__ boffs, uint32_t nb, uint32_t g)
+{
+    uint32_t lo = 0, hi = nb;  // boffs[lo] <= g < boffs[hi]
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (boffs[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+}  // namespace bmh

@@ -1,0 +1,283 @@
+// pack.hip — Huffman bit-pack of a batch of MTF streams into reference records.
+//
+// Replaces encode_with_huffman() + append_bit (reference main.cpp:158-172,
+// io_utilities.h:87-94): code words concatenated MSB-first, the first bit at bit 7 of the
+// payload's first byte. Three steps per block, chunked 4096 symbols per workgroup:
+//   bits   : per chunk, sum of code lengths (code-length table in LDS)
+//   scan   : per block, exclusive scan of chunk bit counts (u64)
+//   write  : per chunk, thread bit offsets by a workgroup scan; code words OR'd into an LDS
+//            image of the chunk's 32-bit big-endian words; interior words stored, the two
+//            edge words (shared with neighbouring chunks / record headers) atomicOr'd.
+// The output region is zeroed first; record headers + tree bytes (host-built) are copied in
+// by k_headers before the pack, and the payload of block b starts at byte pay_offs[b].
+#include "bmh_internal.h"
+#include "device_util.h"
+
+#include <algorithm>
+
+namespace bmh {
+
+namespace {
+
+constexpr uint32_t kPackChunk = 4096;  // symbols per workgroup (256 threads x 16)
+constexpr uint32_t kPackIPT = kPackChunk / 256;
+
+struct DevTable {
+    uint64_t code[256];
+    uint8_t len[256];
+};
+
+struct PChunk {
+    uint32_t block, start, len, pad;
+};
+
+__global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ mtf, const PChunk *__restrict__ chunks,
+                                                   const DevTable *__restrict__ tabs, uint64_t *__restrict__ cbits)
+{
+    __shared__ uint8_t s_len[256];
+    __shared__ uint64_t s_tmp[8];
+    const PChunk ch = chunks[blockIdx.x];
+    s_len[threadIdx.x] = tabs[ch.block].len[threadIdx.x];
+    __syncthreads();
+    uint64_t s = 0;
+    for (uint32_t i = threadIdx.x; i < ch.len; i += 256) s += s_len[mtf[ch.start + i]];
+    uint64_t total;
+    block_excl_sum64<256>(s, s_tmp, &total);
+    if (threadIdx.x == 0) cbits[blockIdx.x] = total;
+}
+
+// grid = nblocks; exclusive scan of the block's chunk bit counts (in place)
+__global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ cfirst, uint64_t *__restrict__ cbits)
+{
+    __shared__ uint64_t s_tmp[8];
+    const uint32_t c0 = cfirst[blockIdx.x], c1 = cfirst[blockIdx.x + 1];
+    uint64_t carry = 0;
+    for (uint32_t base = c0; base < c1; base += 256) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t v = i < c1 ? cbits[i] : 0ull;
+        uint64_t total;
+        const uint64_t ex = block_excl_sum64<256>(v, s_tmp, &total);
+        if (i < c1) cbits[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ mtf, const PChunk *__restrict__ chunks,
+                                                    const DevTable *__restrict__ tabs,
+                                                    const uint64_t *__restrict__ cboff,
+                                                    const uint64_t *__restrict__ pay_offs, uint32_t *__restrict__ out)
+{
+    __shared__ uint64_t s_code[256];
+    __shared__ uint8_t s_len[256];
+    __shared__ uint64_t s_tmp[8];
+    __shared__ uint32_t s_img[kPackChunk * 64 / 32 + 2];
+    const PChunk ch = chunks[blockIdx.x];
+    const DevTable *t = &tabs[ch.block];
+    s_code[threadIdx.x] = t->code[threadIdx.x];
+    s_len[threadIdx.x] = t->len[threadIdx.x];
+    __syncthreads();
+    const uint64_t G = pay_offs[ch.block] * 8 + cboff[blockIdx.x];  // global bit position
+    const uint64_t W0 = G >> 5;
+    const uint32_t sh0 = (uint32_t)(G & 31u);
+    uint8_t sym[kPackIPT];
+    uint64_t mybits = 0;
+    const uint32_t i0 = threadIdx.x * kPackIPT;
+    for (uint32_t k = 0; k < kPackIPT; ++k) {
+        const uint32_t i = i0 + k;
+        sym[k] = i < ch.len ? mtf[ch.start + i] : 0;
+        mybits += i < ch.len ? s_len[sym[k]] : 0u;
+    }
+    uint64_t total;
+    uint64_t tb = block_excl_sum64<256>(mybits, s_tmp, &total) + sh0;
+    if (total == 0) return;
+    const uint32_t nwords = (uint32_t)((sh0 + total + 31) >> 5);
+    for (uint32_t w = threadIdx.x; w < nwords; w += 256) s_img[w] = 0;
+    __syncthreads();
+    for (uint32_t k = 0; k < kPackIPT; ++k) {
+        if (i0 + k >= ch.len) break;
+        uint32_t l = s_len[sym[k]];
+        const uint64_t code = s_code[sym[k]];
+        while (l > 0) {
+            const uint32_t off = (uint32_t)(tb & 31u);
+            const uint32_t take = min(l, 32u - off);
+            const uint32_t bits = (uint32_t)((code >> (l - take)) & ((take == 32) ? 0xffffffffull : ((1ull << take) - 1)));
+            atomicOr(&s_img[tb >> 5], bits << (32u - off - take));
+            tb += take;
+            l -= take;
+        }
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < nwords; w += 256) {
+        const uint32_t v = __builtin_bswap32(s_img[w]);
+        if (w == 0 || w == nwords - 1) atomicOr(&out[W0 + w], v);
+        else out[W0 + w] = v;
+    }
+}
+
+// Standalone histogram + first occurrence (huffman() main.cpp:231-244) for any byte stream.
+__global__ __launch_bounds__(256) void k_histogram(const uint8_t *__restrict__ in, const PChunk *__restrict__ chunks,
+                                                   const uint64_t *__restrict__ boffs, uint32_t *__restrict__ freq,
+                                                   uint32_t *__restrict__ first)
+{
+    __shared__ uint32_t h[256], f[256];
+    const PChunk ch = chunks[blockIdx.x];
+    h[threadIdx.x] = 0;
+    f[threadIdx.x] = 0xffffffffu;
+    __syncthreads();
+    const uint32_t rel0 = (uint32_t)(ch.start - boffs[ch.block]);
+    for (uint32_t i = threadIdx.x; i < ch.len; i += 256) {
+        const uint32_t v = in[ch.start + i];
+        atomicAdd(&h[v], 1u);
+        atomicMin(&f[v], rel0 + i);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) {
+        atomicAdd(&freq[(size_t)ch.block * 256 + threadIdx.x], h[threadIdx.x]);
+        atomicMin(&first[(size_t)ch.block * 256 + threadIdx.x], f[threadIdx.x]);
+    }
+}
+
+__global__ void k_fill(uint32_t *p, uint32_t v, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+// Copy host-built [u64 primary][u64 n][u64 tree_len][tree] prefixes to the record offsets.
+__global__ __launch_bounds__(64) void k_headers(const uint8_t *__restrict__ src, const uint64_t *__restrict__ src_offs,
+                                                const uint64_t *__restrict__ rec_offs, uint8_t *__restrict__ out)
+{
+    const uint32_t b = blockIdx.x;
+    const uint64_t s0 = src_offs[b], len = src_offs[b + 1] - s0;
+    for (uint32_t i = threadIdx.x; i < len; i += 64) out[rec_offs[b] + i] = src[s0 + i];
+}
+
+}  // namespace
+
+void write_headers(Ctx *c, uint8_t *d_out, const std::vector<uint8_t> &hdr_bytes, const std::vector<uint64_t> &src_offs,
+                   const std::vector<uint64_t> &rec_offs)
+{
+    const uint32_t nb = (uint32_t)rec_offs.size() - 1;
+    const size_t hb = hdr_bytes.size();
+    uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, hb + (nb + 1) * 16 + 64);
+    uint64_t *d_src = (uint64_t *)(d_hdr + ((hb + 15) & ~(size_t)15));
+    uint64_t *d_rec = d_src + (nb + 1);
+    BMH_HIP(hipMemcpyAsync(d_hdr, hdr_bytes.data(), hb, hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_src, src_offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_rec, rec_offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    BMH_LAUNCH(c, "pack_headers", k_headers, nb, 64, 0, d_hdr, d_src, d_rec, d_out);
+    c->sync();  // host vectors may be released by the caller
+}
+
+void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32)
+{
+    const uint32_t nb = bt.nblocks;
+    std::vector<PChunk> hc;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
+        for (uint64_t s = 0; s < n; s += 65536) {
+            PChunk p;
+            p.block = b;
+            p.start = (uint32_t)(o + s);
+            p.len = (uint32_t)std::min<uint64_t>(65536, n - s);
+            p.pad = 0;
+            hc.push_back(p);
+        }
+    }
+    const uint32_t nch = (uint32_t)hc.size();
+    uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 8 + 64);
+    PChunk *d_chunks = (PChunk *)d_meta;
+    uint64_t *d_offs = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + 15) & ~(size_t)15));
+    uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
+    uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
+    BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(PChunk), hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_offs, bt.offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
+    BMH_LAUNCH(c, "hist_fill", k_fill, (uint32_t)(((size_t)nb * 256 + 255) / 256), 256, 0, d_first, 0xffffffffu,
+               (size_t)nb * 256);
+    BMH_LAUNCH(c, "histogram", k_histogram, nch, 256, 0, d_in, d_chunks, d_offs, d_freq, d_first);
+    BMH_HIP(hipMemcpyAsync(h_freq32, d_freq, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    BMH_HIP(hipMemcpyAsync(h_first32, d_first, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    c->sync();
+}
+
+void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
+                const uint64_t *pay_offs)
+{
+    if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
+    const uint32_t nb = bt.nblocks;
+    std::vector<DevTable> ht(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        memcpy(ht[b].code, tables[b].code, sizeof ht[b].code);
+        memcpy(ht[b].len, tables[b].len, sizeof ht[b].len);
+        for (int s = 0; s < 256; ++s)
+            if (tables[b].len[s] > 64) fail(BMH_ERANGE, "pack: code longer than 64 bits");
+    }
+    std::vector<PChunk> hc;
+    std::vector<uint32_t> cfirst(nb + 1);
+    for (uint32_t b = 0; b < nb; ++b) {
+        cfirst[b] = (uint32_t)hc.size();
+        const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
+        for (uint64_t s = 0; s < n; s += kPackChunk) {
+            PChunk p;
+            p.block = b;
+            p.start = (uint32_t)(o + s);
+            p.len = (uint32_t)std::min<uint64_t>(kPackChunk, n - s);
+            p.pad = 0;
+            hc.push_back(p);
+        }
+    }
+    cfirst[nb] = (uint32_t)hc.size();
+    const uint32_t nch = (uint32_t)hc.size();
+    DevTable *d_tab = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
+    uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 4 + nb * 8 + 64);
+    PChunk *d_chunks = (PChunk *)d_meta;
+    uint32_t *d_cfirst = (uint32_t *)(d_meta + nch * sizeof(PChunk));
+    uint64_t *d_pay = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + (nb + 1) * 4 + 15) & ~(size_t)15));
+    uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
+    BMH_HIP(hipMemcpyAsync(d_tab, ht.data(), nb * sizeof(DevTable), hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(PChunk), hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_cfirst, cfirst.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_pay, pay_offs, nb * 8, hipMemcpyHostToDevice, c->stream));
+    BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits);
+    BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits, d_pay, (uint32_t *)d_out);
+    c->sync();
+}
+
+// ---------------------------------------------------------------- synthetic input (App. D)
+namespace {
+__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t k)
+{
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_splitmix(uint8_t *__restrict__ out, uint64_t nbytes, uint64_t seed, uint64_t offset)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i0 = t * 8;
+    if (i0 >= nbytes) return;
+    const uint64_t g = offset + i0;
+    const uint64_t w = g >> 3;
+    const uint32_t s = (uint32_t)(g & 7u);
+    const uint64_t z0 = splitmix_word(seed, w);
+    uint64_t v = z0 >> (8 * s);
+    if (s) v |= splitmix_word(seed, w + 1) << (64 - 8 * s);
+    if (i0 + 8 <= nbytes && (((uintptr_t)(out + i0)) & 7u) == 0) {
+        *(uint64_t *)(out + i0) = v;
+    } else {
+        for (uint32_t j = 0; j < 8 && i0 + j < nbytes; ++j) out[i0 + j] = (uint8_t)(v >> (8 * j));
+    }
+}
+}  // namespace
+
+void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset)
+{
+    const uint64_t threads = (nbytes + 7) / 8;
+    BMH_LAUNCH(c, "synth_splitmix64", k_splitmix, (uint32_t)((threads + 255) / 256), 256, 0, d_out, nbytes, seed, offset);
+    c->sync();
+}
+
+}  // namespace bmh

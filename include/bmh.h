@@ -1,0 +1,150 @@
+/*
+ * bmh.h — C ABI of the MI355X-native BWT -> MTF -> Huffman block encoder (libbmh.so).
+ *
+ * The reference (komour/bwt-mtf-huffman-compressor) has no plugin/FFI API: its seam is the
+ * set of free C++ stage functions that compress() calls in sequence (main.cpp:305-316).
+ * Each entry point below replaces one of them (cited), batched over independent blocks and
+ * running on one GPU per context. All functions return a bmh_status; nothing throws.
+ *
+ * Memory: functions named *_dev take device (HBM) pointers allocated with bmh_dev_alloc (or
+ * any hipMalloc'd / torch CUDA tensor memory of the context's device); host arrays are
+ * plain host memory. A "batch" of nblocks blocks is described by `offs`, a HOST array of
+ * nblocks+1 uint64 prefix offsets: block b is bytes [offs[b], offs[b+1]) of the buffer.
+ * Limits: every block 1 <= n < 2^32 - 1; a batch totals < 2^32 bytes (split bigger jobs).
+ *
+ * Threading: a context is used by one host thread at a time (one context per GPU).
+ * All calls are synchronous: they return when their results are complete.
+ */
+#ifndef BMH_H
+#define BMH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    BMH_OK = 0,
+    BMH_EINVAL = 1,   /* bad argument (e.g. empty block: the reference segfaults there) */
+    BMH_ENOMEM = 2,   /* host or device allocation failed */
+    BMH_EHIP = 3,     /* a HIP runtime call failed */
+    BMH_ERANGE = 4,   /* output capacity too small / size limit exceeded */
+    BMH_ECORRUPT = 5, /* malformed record or container */
+    BMH_ENODEV = 6    /* no usable gfx950 device */
+} bmh_status;
+
+typedef struct bmh_ctx bmh_ctx;
+
+/* Per-block Huffman code table: the data the reference keeps in its BTree + the
+ * unordered_map<u8, vector<bool>> of build_hashmap (main.cpp:149-156). */
+typedef struct {
+    uint64_t code[256];  /* code word of symbol s, MSB-first, right-aligned */
+    uint8_t len[256];    /* code length in bits (0 for absent symbols / single-leaf tree) */
+    uint8_t tree[320];   /* preorder tree bytes, tree_to_bytes (main.cpp:174-196) */
+    uint32_t tree_len;   /* ceil((10*leaves - 1) / 8) */
+    uint32_t leaves;     /* number of distinct MTF symbols */
+} bmh_code_table;
+
+/* ---- library / context ------------------------------------------------------------ */
+const char *bmh_version(void);
+const char *bmh_status_str(int status);
+/* Last error message of the calling thread (empty string if none). */
+const char *bmh_last_error(void);
+int bmh_device_count(void);
+bmh_status bmh_ctx_create(int device, bmh_ctx **out);
+void bmh_ctx_destroy(bmh_ctx *ctx);
+/* The context's HIP stream (hipStream_t), for callers that order their own work after it. */
+void *bmh_ctx_stream(bmh_ctx *ctx);
+
+/* Device memory helpers (so FFI callers need no HIP headers). */
+bmh_status bmh_dev_alloc(bmh_ctx *ctx, uint64_t bytes, void **d_ptr);
+bmh_status bmh_dev_free(bmh_ctx *ctx, void *d_ptr);
+bmh_status bmh_memcpy_h2d(bmh_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
+bmh_status bmh_memcpy_d2h(bmh_ctx *ctx, void *h_dst, const void *d_src, uint64_t bytes);
+
+/* ---- stage entry points (device buffers, batched over blocks) --------------------- */
+/* Replaces bwt() (main.cpp:77-91): cyclic-rotation BWT of every block. d_L receives the
+ * last column (same layout as d_in); h_primary[b] = the row of rotation 0
+ * (= number of rotations strictly smaller than rotation 0). */
+bmh_status bmh_bwt_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
+                       uint8_t *d_L, uint64_t *h_primary);
+
+/* Replaces move_to_front() (main.cpp:93-112) plus the histogram and first-occurrence scan
+ * of huffman() (main.cpp:231-244). h_freq and h_first are nblocks*256 arrays (may be NULL):
+ * freq of each MTF symbol, and the block-relative index of its first occurrence
+ * (UINT64_MAX if absent). */
+bmh_status bmh_mtf_dev(bmh_ctx *ctx, const uint8_t *d_L, const uint64_t *offs, uint32_t nblocks,
+                       uint8_t *d_mtf, uint64_t *h_freq, uint64_t *h_first);
+
+/* The histogram + first-occurrence scan of huffman() (main.cpp:231-244) on its own, for an
+ * arbitrary device byte stream (bmh_mtf_dev already returns both for its output). */
+bmh_status bmh_histogram_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
+                             uint64_t *h_freq, uint64_t *h_first);
+
+/* Replaces the tree part of huffman() (main.cpp:245-254), traverse/build_hashmap
+ * (main.cpp:132-156) and tree_to_bytes (main.cpp:174-196). Host-only. Leaves are ordered by
+ * first occurrence; equal frequencies break ties by the reference's heap-address order
+ * under glibc. */
+bmh_status bmh_huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out);
+/* Payload bytes encode_with_huffman (main.cpp:158-172) emits: max(1, ceil(sum freq*len / 8)). */
+uint64_t bmh_payload_bytes(const bmh_code_table *table, const uint64_t freq[256]);
+
+/* Replaces encode_with_huffman() (main.cpp:158-172): MSB-first concatenation of code words.
+ * tables[b] is block b's table; block b's payload is written at d_out + pay_offs[b]
+ * (pay_offs: host array, nblocks entries; the caller sizes each with bmh_payload_bytes). */
+bmh_status bmh_pack_dev(bmh_ctx *ctx, const uint8_t *d_mtf, const uint64_t *offs, uint32_t nblocks,
+                        const bmh_code_table *tables, uint8_t *d_out, const uint64_t *pay_offs);
+
+/* Whole encode (compress(), main.cpp:300-325, minus file I/O): one reference record per
+ * block, [u64 primary][u64 n][u64 tree_len][tree][payload] (io_utilities.h:7-27), written
+ * back to back at d_out. h_rec_offs (nblocks+1 entries) receives the record offsets. */
+bmh_status bmh_encode_blocks_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
+                                 uint8_t *d_out, uint64_t out_cap, uint64_t *h_rec_offs);
+/* Capacity sufficient for one record of an n-byte block. */
+uint64_t bmh_record_bound(uint64_t n);
+
+/* ---- host-buffer convenience (H2D + encode + D2H) ---------------------------------- */
+/* Encodes `in` (n bytes) cut into block_size blocks (block_size 0 or >= n: one block).
+ * One block => exactly the reference record; several => the BMH container (bmh_container_*).
+ * Returns the output size in *out_len. */
+bmh_status bmh_compress_host(bmh_ctx *ctx, const uint8_t *in, uint64_t n, uint64_t block_size,
+                             uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+/* Same, spreading blocks round-robin (block b -> ctxs[b % nctx]) over several contexts
+ * (one per GPU), each driven by its own host thread. */
+bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t *in, uint64_t n,
+                                   uint64_t block_size, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
+uint64_t bmh_compress_bound(uint64_t n, uint64_t block_size);
+
+/* ---- decode (host C++; replaces decompress(), main.cpp:327-345) -------------------- */
+/* Decodes one reference record or one BMH container. *n_out receives the decoded size;
+ * if out is NULL only the size is reported. */
+bmh_status bmh_decompress_host(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
+/* Huffman stage inverse only (huffman_reverse, main.cpp:259-281): record -> MTF stream. */
+bmh_status bmh_record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out);
+
+/* ---- container helpers ------------------------------------------------------------ */
+/* A BMH container is: magic "\xffBMHBLK1" | u64 block_size | u64 nblocks | u64 total_n |
+ * u64 record_len[nblocks] | records (each a verbatim reference record). */
+int bmh_is_container(const uint8_t *in, uint64_t len);
+bmh_status bmh_container_info(const uint8_t *in, uint64_t len, uint64_t *nblocks, uint64_t *total_n);
+/* Pointer/length of record b inside a container. */
+bmh_status bmh_container_record(const uint8_t *in, uint64_t len, uint64_t b, const uint8_t **rec, uint64_t *rec_len);
+
+/* ---- measurement ------------------------------------------------------------------- */
+/* When enabled, every kernel launch of the context is bracketed by HIP events on the
+ * context's stream; stats accumulate per kernel name. */
+bmh_status bmh_ctx_set_timing(bmh_ctx *ctx, int enable);
+bmh_status bmh_ctx_reset_stats(bmh_ctx *ctx);
+/* Kernel stats: returns how many distinct kernels were recorded; fills up to cap entries. */
+int bmh_ctx_kernel_stats(bmh_ctx *ctx, char (*names)[64], uint64_t *launches, double *total_ms, int cap);
+
+/* Synthetic input: bytes [offset, offset+nbytes) of the little-endian
+ * splitmix64(seed) stream, generated on the device. */
+bmh_status bmh_synth_splitmix64_dev(bmh_ctx *ctx, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
