@@ -1,26 +1,28 @@
 // bwt.hip — cyclic-rotation BWT of a batch of blocks on gfx950.
 //
 // Replaces bwt() + bwt_cmp_straight + cyclic_index (reference main.cpp:38-59, 77-91), which
-// std::stable_sort's rotation indices with an O(LCP) byte comparator. Here the same order is
-// built by prefix doubling on cyclic ranks:
+// std::stable_sort's rotation indices with an O(LCP) byte comparator. The same order is built
+// here by radix-sorting rotation prefixes, then prefix doubling on cyclic ranks for whatever
+// is still tied:
 //
-//   rank_D[p] = number of rotations whose first D bytes are strictly smaller than those of
-//   rotation p ("group start"). Sorting a depth-D group by rank_D[(p + D) mod n] yields
-//   depth 2D. Identical rotations never split; they stop once D >= n (their L bytes are
-//   equal, and the primary index is rank[0] = count of strictly smaller rotations, exactly
-//   the row std::stable_sort gives rotation 0).
-//
-// Rounds over the whole batch (all blocks progress together, one segment list):
-//   bucket  : LDS-histogram counting sort of every position by its first 2 bytes   -> D = 2
-//   round 1 : every bucket of >= 2 positions sorted by the next 4 data bytes       -> D = 6
-//   round r : every unresolved group sorted by rank_D[(p+D) mod n]                  -> D = 2D
-// Segments are sorted by size class: tiny (<= 128: packed into ~1K-element tiles, rank by
-// counting in LDS), medium (<= 4096: one workgroup, LDS LSD radix), large (global MSD radix
-// passes, 8 bits each, splitting into sub-segments that re-enter the classes).
-//
-// Rank arrays are double buffered (rk_cur read, rk_nxt written) so that keys gathered inside
-// the sort kernels never see this round's updates; elements that resolve in round >= 2 are
-// committed to both arrays after the round (resolved list).
+// Data phase (no rank arrays touched):
+//   global pass : counting sort of every position by the first 12 bits of its rotation
+//                 (4096 buckets per block; LDS histograms; chunks of one block mapped to one
+//                 XCD so the block's bytes and SA write frontier stay in that XCD's L2).
+//   finish      : one workgroup per bucket of <= 4096 positions (bit depth db): LDS counting
+//                 sort by the next 8 bits, then every sub-bucket of <= 64 is ordered by the
+//                 next 32 bits by rank counting (bit depth db + 40). Resolved slots get their
+//                 SA entry AND their last-column byte L[r] = data[(SA[r]+n-1) mod n] here.
+//                 Bigger sub-buckets are deferred to another finish pass at db + 8.
+//   MSD passes  : buckets / sub-buckets larger than 4096 are split by 8 more bits per global
+//                 pass (tile histograms, per-segment scan, scatter) until they fit.
+// Doubling phase (only blocks that still hold tied groups, e.g. text or periodic input):
+//   lazy rank fill: rank[p] = slot of p, or its group's start slot (ranks = #strictly smaller
+//   rotations at the current depth); then rounds sorting each tied group by
+//   rank_D[(p + D) mod n] -> depth 2D (tiny / medium / large-MSD segment classes). Identical
+//   rotations stop once D >= n: their L bytes are equal, and the primary index is the group
+//   start, i.e. the count of strictly smaller rotations — exactly the row std::stable_sort
+//   gives rotation 0.
 #include "bmh_internal.h"
 #include "device_util.h"
 
@@ -30,17 +32,34 @@ namespace bmh {
 
 namespace {
 
-constexpr uint32_t kHistChunk = 4u << 20;   // positions per bucket-histogram chunk
-constexpr uint32_t kHalfBins = 32768;       // 16-bit digit space split in two LDS halves
+// ---------------------------------------------------------------------------- constants
+constexpr uint32_t kGBits = 12;                 // global pass digit width
+constexpr uint32_t kGBins = 1u << kGBits;       // 4096 buckets per block
+constexpr uint32_t kGChunk = 65536;             // positions per global-pass workgroup
+constexpr uint32_t kFinCap = 4096;              // max segment a finish workgroup sorts
+constexpr uint32_t kFinNT = 256, kFinIPT = kFinCap / kFinNT;
+constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
+constexpr uint32_t kFinKeyBits = 40;            // bits consumed by one finish pass (8 + 32)
+constexpr uint32_t kDataMaxBits = 64;           // deeper ties go to rank doubling
+constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
+// doubling phase
 constexpr uint32_t kTinyMax = 128;
 constexpr uint32_t kTileT = 1024;
 constexpr uint32_t kTileCap = kTileT + kTinyMax;  // 1152
 constexpr uint32_t kTileSegMax = kTileCap / 2;
 constexpr uint32_t kMedMax = 4096;
-constexpr uint32_t kLargeTile = 4096;
+constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
-    uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;
+    uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
+    uint32_t fin_next, big_next, big, dgroups, dmin_bits, pad0, pad1, pad2;  // data phase
+};
+
+// Data-phase segment / group: {gstart (batch slot), len, bit depth, block (| kFinalFlag)}
+using Seg4 = uint4;
+
+struct GChunk {
+    uint32_t block, start, len, pad;  // start: block-relative position
 };
 
 struct LSeg {
@@ -50,170 +69,435 @@ struct LTile {
     uint32_t seg, start, len, pad;
 };
 
+struct DataArgs {
+    const uint8_t *data;
+    const uint32_t *boffs;
+    uint32_t nb;
+    uint32_t *sa;
+    uint8_t *L;
+    uint32_t *prim;
+    uint32_t *bflag;   // block keeps tied groups -> needs the rank phase
+    Seg4 *groups;      // tied groups (unresolved or final)
+    Seg4 *fin_next;    // deferred finish segments
+    Seg4 *big_next;    // MSD segments for the next pass
+    Counters *cnt;
+};
+
+__device__ __forceinline__ uint8_t lastcol_byte(const uint8_t *blk, uint32_t n, uint32_t p)
+{
+    return blk[p == 0 ? n - 1 : p - 1];
+}
+
+// Resolved slot: SA, L and (for rotation 0) the primary index. gslot is a batch slot.
+__device__ __forceinline__ void put_final(const DataArgs &a, uint32_t b, uint32_t boff, uint32_t n,
+                                          const uint8_t *blk, uint32_t gslot, uint32_t p, uint32_t rank_local)
+{
+    a.L[gslot] = lastcol_byte(blk, n, p);
+    if (p == 0) a.prim[b] = rank_local;
+}
+
+// Bits [db, db + 64) of rotation p (MSB first), cyclic.
+__device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, uint32_t n, uint32_t p, uint32_t db)
+{
+    const uint32_t B = db >> 3, sh = db & 7u;
+    uint64_t w = 0;
+    uint32_t x;
+    if ((uint64_t)p + B + 9 <= n) {
+        const uint8_t *q = blk + p + B;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w = (w << 8) | q[i];
+        x = q[8];
+    } else {
+        uint64_t s = ((uint64_t)p + B) % n;
+        for (int i = 0; i < 8; ++i) {
+            w = (w << 8) | blk[s];
+            if (++s == n) s = 0;
+        }
+        x = blk[s];
+    }
+    if (sh) w = (w << sh) | (x >> (8 - sh));
+    return w;
+}
+
+// ------------------------------------------------------------------- global 12-bit pass
+__device__ __forceinline__ uint32_t digit12(const uint8_t *__restrict__ blk, uint32_t n, uint32_t p)
+{
+    const uint32_t q = p + 1 == n ? 0 : p + 1;
+    return ((uint32_t)blk[p] << 4) | (blk[q] >> 4);
+}
+
+// grid = chunk list (XCD-interleaved; pad entries have len 0); 1024 threads.
+__global__ __launch_bounds__(1024) void k_g12_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
+                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
+{
+    __shared__ uint32_t h[kGBins];
+    const GChunk ch = chunks[blockIdx.x];
+    if (ch.len == 0) return;
+    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) h[i] = 0;
+    __syncthreads();
+    const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
+    const uint8_t *blk = data + boff;
+    for (uint32_t e = threadIdx.x; e < ch.len; e += 1024) atomicAdd(&h[digit12(blk, n, ch.start + e)], 1u);
+    __syncthreads();
+    uint32_t *out = chist + (size_t)blockIdx.x * kGBins;
+    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) out[i] = h[i];
+}
+
+// grid = nblocks; 1024 threads. Per digit: exclusive prefix over the block's chunks (in place,
+// -> block-relative write offsets), bucket table bk[b][d] = {start, len}; buckets larger than
+// a finish workgroup go to the MSD list.
+__global__ __launch_bounds__(1024) void k_g12_scan(const uint32_t *__restrict__ boffs, uint32_t nb,
+                                                   const uint32_t *__restrict__ bchunks, const uint32_t *__restrict__ bchunk0,
+                                                   uint32_t *__restrict__ chist, uint2 *__restrict__ bk, Seg4 *big,
+                                                   Counters *cnt)
+{
+    __shared__ uint32_t s_tmp[17];
+    const uint32_t b = blockIdx.x;
+    const uint32_t boff = boffs[b];
+    const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // chunk list indices c0 + 8k (XCD lane stride)
+    uint32_t carry = 0;
+    for (uint32_t r = 0; r < kGBins / 1024; ++r) {
+        const uint32_t d = r * 1024 + threadIdx.x;
+        uint32_t tot = 0;
+        for (uint32_t k = 0; k < nc; ++k) tot += chist[(size_t)(c0 + 8 * k) * kGBins + d];
+        uint32_t total;
+        const uint32_t start = carry + block_excl_sum<1024>(tot, s_tmp, &total);
+        uint32_t acc = start;
+        for (uint32_t k = 0; k < nc; ++k) {
+            uint32_t *h = &chist[(size_t)(c0 + 8 * k) * kGBins + d];
+            const uint32_t v = *h;
+            *h = acc;
+            acc += v;
+        }
+        bk[(size_t)b * kGBins + d] = make_uint2(start, tot);
+        if (tot > kFinCap) big[atomicAdd(&cnt->big, 1u)] = make_uint4(boff + start, tot, kGBits, b);
+        carry += total;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_g12_scatter(DataArgs a, const GChunk *__restrict__ chunks,
+                                                      const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk)
+{
+    __shared__ uint32_t cur[kGBins];
+    const GChunk ch = chunks[blockIdx.x];
+    if (ch.len == 0) return;
+    const uint32_t *in = chist + (size_t)blockIdx.x * kGBins;
+    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) cur[i] = in[i];
+    __syncthreads();
+    const uint32_t b = ch.block;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    const uint2 *bkb = bk + (size_t)b * kGBins;
+    for (uint32_t e = threadIdx.x; e < ch.len; e += 1024) {
+        const uint32_t p = ch.start + e;
+        const uint32_t d = digit12(blk, n, p);
+        const uint32_t slot = atomicAdd(&cur[d], 1u);
+        a.sa[boff + slot] = p;
+        if (bkb[d].y == 1) put_final(a, b, boff, n, blk, boff + slot, p, slot);  // singleton bucket
+    }
+}
+
+// ------------------------------------------------------------------------- finish pass
+// dense = 1: workgroup i -> (block, bucket) of the global pass, XCD-aware (i % 8 = lane of
+// blocks b = lane mod 8). dense = 0: one workgroup per list entry.
+__global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restrict__ list, const uint2 *__restrict__ bk,
+                                                int dense)
+{
+    __shared__ uint32_t s_pos[kFinCap], s_rest[kFinCap];
+    __shared__ uint8_t s_dig[kFinCap];
+    __shared__ uint32_t s_cnt[256], s_start[257];
+    __shared__ uint32_t s_tmp[8];
+    uint32_t gstart, len, db, b;
+    if (dense) {
+        const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
+        b = x + 8u * (k >> kGBits);
+        if (b >= a.nb) return;
+        const uint2 e = bk[(size_t)b * kGBins + (k & (kGBins - 1))];
+        len = e.y;
+        if (len < 2 || len > kFinCap) return;
+        gstart = a.boffs[b] + e.x;
+        db = kGBits;
+    } else {
+        const Seg4 s = list[blockIdx.x];
+        gstart = s.x;
+        len = s.y;
+        db = s.z;
+        b = s.w;
+    }
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    const uint32_t tid = threadIdx.x;
+    s_cnt[tid] = 0;
+    __syncthreads();
+    uint32_t pv[kFinIPT], rv[kFinIPT], dv[kFinIPT];
+#pragma unroll
+    for (uint32_t k = 0; k < kFinIPT; ++k) {
+        const uint32_t e = tid + k * kFinNT;
+        if (e < len) {
+            const uint32_t p = a.sa[gstart + e];
+            const uint64_t w = rot_window(blk, n, p, db);
+            pv[k] = p;
+            dv[k] = (uint32_t)(w >> 56);
+            rv[k] = (uint32_t)(w >> 24);
+            atomicAdd(&s_cnt[dv[k]], 1u);
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t c = s_cnt[tid];
+        const uint32_t ex = block_excl_sum<kFinNT>(c, s_tmp, nullptr);
+        s_start[tid] = ex;
+        if (tid == kFinNT - 1) s_start[256] = ex + c;
+        __syncthreads();
+        s_cnt[tid] = ex;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kFinIPT; ++k) {
+        const uint32_t e = tid + k * kFinNT;
+        if (e < len) {
+            const uint32_t dst = atomicAdd(&s_cnt[dv[k]], 1u);
+            s_pos[dst] = pv[k];
+            s_rest[dst] = rv[k];
+            s_dig[dst] = (uint8_t)dv[k];
+        }
+    }
+    __syncthreads();
+    const uint64_t newbits = (uint64_t)db + kFinKeyBits;
+    const bool final_depth = newbits >= 8ull * n;
+    for (uint32_t e = tid; e < len; e += kFinNT) {
+        const uint32_t d = s_dig[e];
+        const uint32_t s0 = s_start[d], m = s_start[d + 1] - s0;
+        const uint32_t p = s_pos[e];
+        if (m == 1) {
+            a.sa[gstart + s0] = p;
+            put_final(a, b, boff, n, blk, gstart + s0, p, gstart + s0 - boff);
+        } else if (m > kSmallM) {
+            a.sa[gstart + e] = p;  // deferred, still grouped by the 8-bit digit
+            if (e == s0) {
+                const uint32_t nd = db + 8;
+                if (nd < 8ull * n)
+                    a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gstart + s0, m, nd, b);
+                else
+                    a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gstart + s0, m, nd, b | kFinalFlag);
+            }
+        } else {
+            const uint32_t r = s_rest[e];
+            uint32_t lt = 0, eqb = 0, eqt = 0;
+            for (uint32_t f = s0; f < s0 + m; ++f) {
+                const uint32_t rf = s_rest[f];
+                lt += rf < r;
+                const bool eq = rf == r;
+                eqt += eq;
+                eqb += eq && f < e;
+            }
+            const uint32_t slot = gstart + s0 + lt + eqb;
+            a.sa[slot] = p;
+            const uint32_t gs = gstart + s0 + lt;
+            if (eqt == 1) {
+                put_final(a, b, boff, n, blk, slot, p, slot - boff);
+            } else {
+                if (final_depth) put_final(a, b, boff, n, blk, slot, p, gs - boff);
+                if (eqb == 0) {
+                    a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
+                        make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
+                    if (!final_depth) a.bflag[b] = 1;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------- MSD passes on data bits
+struct DTile {
+    uint32_t seg, start, len, pad;
+};
+
+__global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                               uint32_t *__restrict__ thist)
+{
+    __shared__ uint32_t h[256];
+    const DTile t = tiles[blockIdx.x];
+    const Seg4 s = segs[t.seg];
+    const uint32_t boff = a.boffs[s.w], n = a.boffs[s.w + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < t.len; e += 256)
+        atomicAdd(&h[(uint32_t)(rot_window(blk, n, a.sa[t.start + e], s.z) >> 56)], 1u);
+    __syncthreads();
+    thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// grid = nsegs; 256 threads (digits). Offsets in place; sub-segment routing.
+__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint2 *__restrict__ segtiles,
+                                               uint32_t *__restrict__ thist, uint32_t *__restrict__ stot,
+                                               uint32_t *__restrict__ nomove)
+{
+    __shared__ uint32_t s_tmp[8];
+    const Seg4 s = segs[blockIdx.x];
+    const uint2 tr = segtiles[blockIdx.x];
+    const uint32_t d = threadIdx.x;
+    uint32_t run = 0;
+    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
+        const uint32_t v = thist[(size_t)t * 256 + d];
+        thist[(size_t)t * 256 + d] = run;
+        run += v;
+    }
+    const uint32_t tot = run;
+    const int nz = __syncthreads_count(tot > 0);
+    const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
+    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
+    stot[(size_t)blockIdx.x * 256 + d] = tot;
+    const uint32_t b = s.w, n = a.boffs[b + 1] - a.boffs[b];
+    const uint32_t nd = s.z + 8;
+    const bool final_depth = (uint64_t)nd >= 8ull * n;
+    auto route = [&](uint32_t gs, uint32_t len) {
+        if (len == 1) return;  // resolved by the scatter
+        if (final_depth || nd >= kDataMaxBits) {
+            a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u));
+            if (!final_depth) a.bflag[b] = 1;
+        } else if (len <= kFinCap) {
+            a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gs, len, nd, b);
+        } else {
+            a.big_next[atomicAdd(&a.cnt->big_next, 1u)] = make_uint4(gs, len, nd, b);
+        }
+    };
+    if (nz == 1) {
+        if (d == 0) nomove[blockIdx.x] = 1;
+        if (tot > 0) route(s.x, s.y);
+    } else {
+        if (d == 0) nomove[blockIdx.x] = 0;
+        if (tot > 0) route(s.x + base, tot);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                                  const uint32_t *__restrict__ nomove, const uint32_t *__restrict__ thist,
+                                                  const uint32_t *__restrict__ stot, uint32_t *__restrict__ sa2)
+{
+    __shared__ uint32_t cur[256];
+    const DTile t = tiles[blockIdx.x];
+    const Seg4 s = segs[t.seg];
+    const uint32_t b = s.w, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    if (nomove[t.seg]) return;  // one digit only: nothing moves
+    cur[threadIdx.x] = thist[(size_t)blockIdx.x * 256 + threadIdx.x];
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+        const uint32_t j = t.start + e;
+        const uint32_t p = a.sa[j];
+        const uint32_t d = (uint32_t)(rot_window(blk, n, p, s.z) >> 56);
+        const uint32_t slot = atomicAdd(&cur[d], 1u);
+        sa2[slot] = p;
+        if (stot[(size_t)t.seg * 256 + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dcopy(const DTile *__restrict__ tiles, const uint32_t *__restrict__ nomove,
+                                               uint32_t *__restrict__ sa, const uint32_t *__restrict__ sa2)
+{
+    const DTile t = tiles[blockIdx.x];
+    if (nomove[t.seg]) return;
+    for (uint32_t e = threadIdx.x; e < t.len; e += 256) sa[t.start + e] = sa2[t.start + e];
+}
+
+// -------------------------------------------------------------------- lazy rank fill
+// rank[p] = slot of p for every slot of a flagged block (both rank buffers).
+__global__ __launch_bounds__(256) void k_rank_fill(const uint32_t *__restrict__ boffs, const uint32_t *__restrict__ bflag,
+                                                   const uint32_t *__restrict__ sa, uint32_t *__restrict__ rkA,
+                                                   uint32_t *__restrict__ rkB)
+{
+    const uint32_t b = blockIdx.y;
+    if (!bflag[b]) return;
+    const uint32_t boff = boffs[b], n = boffs[b + 1] - boff;
+    const uint32_t j0 = blockIdx.x * 4096u;
+    if (j0 >= n) return;
+    const uint32_t j1 = min(j0 + 4096u, n);
+    for (uint32_t j = j0 + threadIdx.x; j < j1; j += 256) {
+        const uint32_t p = sa[boff + j];
+        rkA[boff + p] = j;
+        rkB[boff + p] = j;
+    }
+}
+
+// Tied groups of the data phase: members get the group start as rank (flagged blocks);
+// identical-rotation (final) groups also get their L bytes / primary. Unresolved ones are
+// appended to the first doubling round's segment list. One wave per group.
+__global__ __launch_bounds__(256) void k_group_fill(DataArgs a, const Seg4 *__restrict__ groups, uint32_t ng,
+                                                    uint32_t *__restrict__ rkA, uint32_t *__restrict__ rkB,
+                                                    uint2 *__restrict__ segs, Counters *cnt)
+{
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t l = threadIdx.x & 63u;
+    for (uint32_t g = wave; g < ng; g += nwaves) {
+        const Seg4 s = groups[g];
+        const uint32_t b = s.w & ~kFinalFlag;
+        const bool fin = (s.w & kFinalFlag) != 0;
+        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+        const uint8_t *blk = a.data + boff;
+        const bool ranks = a.bflag[b] != 0;
+        for (uint32_t e = l; e < s.y; e += 64) {
+            const uint32_t p = a.sa[s.x + e];
+            if (ranks) {
+                rkA[boff + p] = s.x - boff;
+                rkB[boff + p] = s.x - boff;
+            }
+            if (fin) put_final(a, b, boff, n, blk, s.x + e, p, s.x - boff);
+        }
+        if (!fin && l == 0) {
+            segs[atomicAdd(&cnt->next, 1u)] = make_uint2(s.x, s.y);
+            atomicMin(&cnt->dmin_bits, s.z);
+        }
+    }
+}
+
+// ======================================================================= doubling phase
 struct RoundArgs {
     const uint8_t *data;
     const uint32_t *boffs;
     uint32_t nb;
     uint32_t *sa;
+    uint8_t *L;
+    uint32_t *prim;
     const uint32_t *rk_cur;
     uint32_t *rk_nxt;
-    uint32_t *rkA, *rkB;
-    uint32_t D;          // current depth (key = rank_D at p + D) — unused in round 1
+    uint32_t D;          // current depth in bytes (key = rank_D at p + D)
     uint64_t newD;       // depth reached by this round
-    int round1;          // key = 4 data bytes at p+2 (D = 2 -> 6)
     uint2 *next;
-    uint32_t *resolved;  // round >= 2: positions resolved this round (global slot of p)
+    uint32_t *resolved;  // positions resolved this round (batch index of p) -> committed after
     Counters *cnt;
 };
 
-__device__ __forceinline__ uint32_t key_data4(const uint8_t *__restrict__ blk, uint32_t n, uint32_t p)
-{
-    if ((uint64_t)p + 5 < n) {
-        return ((uint32_t)blk[p + 2] << 24) | ((uint32_t)blk[p + 3] << 16) | ((uint32_t)blk[p + 4] << 8) |
-               (uint32_t)blk[p + 5];
-    }
-    uint32_t k = 0;
-    for (int i = 0; i < 4; ++i) k = (k << 8) | blk[(uint32_t)(((uint64_t)p + 2 + i) % n)];
-    return k;
-}
-
 __device__ __forceinline__ uint32_t round_key(const RoundArgs &a, uint32_t boff, uint32_t n, uint32_t p)
 {
-    if (a.round1) return key_data4(a.data + boff, n, p);
     uint64_t q = (uint64_t)p + (a.D % n);
     if (q >= n) q -= n;
     return a.rk_cur[boff + (uint32_t)q];
 }
 
-// Rank bookkeeping for element p (block-local) of a depth-newD group starting at block-local
-// slot gs with gsz members; `first` marks one member per group (emits it for the next round).
-__device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32_t n, uint32_t p, uint32_t gs,
-                                       uint32_t gsz, bool first)
+// Element p (block-local) now at batch slot gslot, in a depth-newD group starting at
+// block-local slot gs with gsz members; `first` marks one member per group.
+__device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32_t n, uint32_t p, uint32_t gslot,
+                                       uint32_t gs, uint32_t gsz, bool first)
 {
     const bool final_ = gsz == 1 || a.newD >= n;
+    a.rk_nxt[boff + p] = gs;
     if (final_) {
-        if (a.round1) {
-            a.rkA[boff + p] = gs;
-            a.rkB[boff + p] = gs;
-        } else {
-            a.rk_nxt[boff + p] = gs;
-            uint32_t i = atomicAdd(&a.cnt->resolved, 1u);
-            a.resolved[i] = boff + p;
+        const uint32_t i = atomicAdd(&a.cnt->resolved, 1u);
+        a.resolved[i] = boff + p;
+        a.L[gslot] = a.data[boff + (p == 0 ? n - 1 : p - 1)];
+        if (p == 0) {
+            const uint32_t b = find_block(a.boffs, a.nb, boff);
+            a.prim[b] = gs;
         }
-    } else {
-        a.rk_nxt[boff + p] = gs;
-        if (first) {
-            uint32_t i = atomicAdd(&a.cnt->next, 1u);
-            a.next[i] = make_uint2(boff + gs, gsz);
-        }
+    } else if (first) {
+        const uint32_t i = atomicAdd(&a.cnt->next, 1u);
+        a.next[i] = make_uint2(boff + gs, gsz);
     }
 }
 
-// ------------------------------------------------------------------ bucket round (D = 2)
-__device__ __forceinline__ uint32_t digit16(const uint8_t *__restrict__ blk, uint32_t n, uint32_t p)
-{
-    uint32_t q = p + 1 == n ? 0 : p + 1;
-    return ((uint32_t)blk[p] << 8) | blk[q];
-}
-
-// grid = chunks*2 (chunk, half); 1024 threads; dynamic LDS = 32768 u32 counters.
-__global__ __launch_bounds__(1024) void k_bucket_hist(const uint8_t *__restrict__ data,
-                                                      const BlockInfo *__restrict__ blocks,
-                                                      const uint32_t *__restrict__ chunk_block,
-                                                      const uint32_t *__restrict__ chunk_first,
-                                                      uint32_t *__restrict__ chist)
-{
-    extern __shared__ uint32_t cnt[];
-    const uint32_t chunk = blockIdx.x >> 1, half = blockIdx.x & 1;
-    const uint32_t b = chunk_block[chunk];
-    const BlockInfo bi = blocks[b];
-    const uint32_t c = chunk - chunk_first[b];
-    const uint32_t p0 = c * kHistChunk;
-    const uint32_t p1 = min(p0 + kHistChunk, bi.n);
-    for (uint32_t i = threadIdx.x; i < kHalfBins; i += blockDim.x) cnt[i] = 0;
-    __syncthreads();
-    const uint8_t *blk = data + bi.off;
-    for (uint32_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        uint32_t d = digit16(blk, bi.n, p);
-        if ((d >> 15) == half) atomicAdd(&cnt[d & (kHalfBins - 1)], 1u);
-    }
-    __syncthreads();
-    uint32_t *out = chist + (size_t)blockIdx.x * kHalfBins;
-    for (uint32_t i = threadIdx.x; i < kHalfBins; i += blockDim.x) out[i] = cnt[i];
-}
-
-// grid = nblocks; 1024 threads. Bucket totals -> starts (bstart[b][0..65536]); per-chunk
-// histograms become per-chunk write offsets; buckets of >= 2 positions become segments.
-__global__ __launch_bounds__(1024) void k_bucket_scan(const BlockInfo *__restrict__ blocks,
-                                                      const uint32_t *__restrict__ chunk_first,
-                                                      uint32_t *__restrict__ chist, uint32_t *__restrict__ bstart,
-                                                      uint2 *__restrict__ segs, Counters *cnt)
-{
-    __shared__ uint32_t s_tmp[17];
-    const uint32_t b = blockIdx.x;
-    const BlockInfo bi = blocks[b];
-    const uint32_t c0 = chunk_first[b], nc = chunk_first[b + 1] - c0;
-    uint32_t carry = 0;
-    uint32_t *bs = bstart + (size_t)b * 65537;
-    for (uint32_t r = 0; r < 64; ++r) {
-        const uint32_t d = r * 1024 + threadIdx.x;
-        const uint32_t half = d >> 15, idx = d & (kHalfBins - 1);
-        uint32_t tot = 0;
-        for (uint32_t c = 0; c < nc; ++c) tot += chist[((size_t)(c0 + c) * 2 + half) * kHalfBins + idx];
-        uint32_t total;
-        uint32_t ex = block_excl_sum<1024>(tot, s_tmp, &total);
-        const uint32_t start = carry + ex;
-        bs[d] = start;
-        uint32_t acc = start;
-        for (uint32_t c = 0; c < nc; ++c) {
-            uint32_t *h = &chist[((size_t)(c0 + c) * 2 + half) * kHalfBins + idx];
-            uint32_t v = *h;
-            *h = acc;
-            acc += v;
-        }
-        if (tot >= 2 && bi.n > 2) {
-            uint32_t i = atomicAdd(&cnt->next, 1u);
-            segs[i] = make_uint2(bi.off + start, tot);
-        }
-        carry += total;
-    }
-    if (threadIdx.x == 0) bs[65536] = bi.n;
-}
-
-__global__ __launch_bounds__(1024) void k_bucket_scatter(const uint8_t *__restrict__ data,
-                                                         const BlockInfo *__restrict__ blocks,
-                                                         const uint32_t *__restrict__ chunk_block,
-                                                         const uint32_t *__restrict__ chunk_first,
-                                                         const uint32_t *__restrict__ chist,
-                                                         const uint32_t *__restrict__ bstart, uint32_t *__restrict__ sa,
-                                                         uint32_t *__restrict__ rkA, uint32_t *__restrict__ rkB)
-{
-    extern __shared__ uint32_t cur[];
-    const uint32_t chunk = blockIdx.x >> 1, half = blockIdx.x & 1;
-    const uint32_t b = chunk_block[chunk];
-    const BlockInfo bi = blocks[b];
-    const uint32_t c = chunk - chunk_first[b];
-    const uint32_t p0 = c * kHistChunk;
-    const uint32_t p1 = min(p0 + kHistChunk, bi.n);
-    const uint32_t *in = chist + (size_t)blockIdx.x * kHalfBins;
-    for (uint32_t i = threadIdx.x; i < kHalfBins; i += blockDim.x) cur[i] = in[i];
-    __syncthreads();
-    const uint8_t *blk = data + bi.off;
-    const uint32_t *bs = bstart + (size_t)b * 65537;
-    for (uint32_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        uint32_t d = digit16(blk, bi.n, p);
-        if ((d >> 15) != half) continue;
-        uint32_t slot = atomicAdd(&cur[d & (kHalfBins - 1)], 1u);
-        sa[bi.off + slot] = p;
-        uint32_t st = bs[d];
-        if (bs[d + 1] - st == 1 || bi.n <= 2) {  // resolved (or final: D = 2 >= n)
-            rkA[bi.off + p] = st;
-            rkB[bi.off + p] = st;
-        }
-    }
-}
-
-// ------------------------------------------------------------------------- classification
 __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 *__restrict__ tiny,
                            uint2 *__restrict__ med, LSeg *__restrict__ large, Counters *cnt)
 {
@@ -255,10 +539,10 @@ __global__ __launch_bounds__(1024) void k_scan_partials(uint32_t *__restrict__ p
     __shared__ uint32_t s_tmp[17];
     uint32_t carry = 0;
     for (uint32_t base = 0; base < n; base += 1024) {
-        uint32_t i = base + threadIdx.x;
-        uint32_t v = i < n ? partials[i] : 0u;
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < n ? partials[i] : 0u;
         uint32_t total;
-        uint32_t ex = block_excl_sum<1024>(v, s_tmp, &total);
+        const uint32_t ex = block_excl_sum<1024>(v, s_tmp, &total);
         if (i < n) partials[i] = carry + ex;
         carry += total;
     }
@@ -290,7 +574,6 @@ __global__ void k_tile_heads(const uint32_t *__restrict__ prefix, uint32_t n, ui
     if (i == 0 || prefix[i - 1] / kTileT != t) tiles[atomicAdd(&cnt->tiles, 1u)] = i;
 }
 
-// ------------------------------------------------------------------------------ tiny tiles
 // One workgroup per tile of consecutive tiny segments (<= 1152 elements). Each element's new
 // slot = segment start + #(keys < mine) + #(equal keys before me); group = equal keys.
 __global__ __launch_bounds__(256) void k_tiny(RoundArgs a, const uint2 *__restrict__ tiny, uint32_t ntiny,
@@ -345,13 +628,13 @@ __global__ __launch_bounds__(256) void k_tiny(RoundArgs a, const uint2 *__restri
             eqb += eq && f < e;
         }
         const uint32_t p = s_pos[e];
-        a.sa[s_gstart[k] + lt + eqb] = p;
+        const uint32_t slot = s_gstart[k] + lt + eqb;
+        a.sa[slot] = p;
         const uint32_t boff = s_boff[k];
-        finish(a, boff, s_n[k], p, s_gstart[k] - boff + lt, eqt, eqb == 0);
+        finish(a, boff, s_n[k], p, slot, s_gstart[k] - boff + lt, eqt, eqb == 0);
     }
 }
 
-// ----------------------------------------------------------------------- medium segments
 // One workgroup per segment of 129..4096 elements: LSD radix sort (4-bit digits, constant
 // digits skipped) in LDS, then equal-key groups via block max / suffix-min scans.
 constexpr int kMedNT = 256, kMedIPT = kMedMax / kMedNT;
@@ -392,10 +675,7 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
         __syncthreads();
         for (int i = 0; i < kMedIPT; ++i) {
             const uint32_t idx = tid * kMedIPT + i;
-            if (idx < m) {
-                const uint32_t d = (s_k[cur][idx] >> sh) & 15u;
-                s_cnt[d * kMedNT + tid]++;
-            }
+            if (idx < m) s_cnt[((s_k[cur][idx] >> sh) & 15u) * kMedNT + tid]++;
         }
         __syncthreads();
         uint32_t loc[16], s = 0;
@@ -413,8 +693,7 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
             const uint32_t idx = tid * kMedIPT + i;
             if (idx < m) {
                 const uint32_t k = s_k[cur][idx];
-                const uint32_t d = (k >> sh) & 15u;
-                const uint32_t pos = s_cnt[d * kMedNT + tid]++;
+                const uint32_t pos = s_cnt[((k >> sh) & 15u) * kMedNT + tid]++;
                 s_k[cur ^ 1][pos] = k;
                 s_v[cur ^ 1][pos] = s_v[cur][idx];
             }
@@ -422,7 +701,6 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
         __syncthreads();
         cur ^= 1;
     }
-    // groups: start = last head at or before e, end = first head after e
     uint32_t hmax = 0, hmin = m;
     for (int i = 0; i < kMedIPT; ++i) {
         const uint32_t e = tid * kMedIPT + i;
@@ -447,12 +725,12 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
         const uint32_t gs = gsa[i], gz = nxt - gs;
         const uint32_t p = s_v[cur][e];
         a.sa[sg.x + e] = p;
-        finish(a, boff, n, p, sg.x - boff + gs, gz, e == gs);
+        finish(a, boff, n, p, sg.x + e, sg.x - boff + gs, gz, e == gs);
         if (e == gs) nxt = e;
     }
 }
 
-// ------------------------------------------------------------------------ large segments
+// Large segments of the doubling phase: global MSD passes on the 32-bit rank key.
 __global__ __launch_bounds__(256) void k_lhist(RoundArgs a, const LSeg *__restrict__ lsegs,
                                                const LTile *__restrict__ tiles, uint32_t *__restrict__ key,
                                                uint32_t *__restrict__ thist)
@@ -500,7 +778,6 @@ __device__ __forceinline__ void push_sub(uint32_t gstart, uint32_t len, uint32_t
     }
 }
 
-// grid = nlseg; 256 threads (= digits)
 __global__ __launch_bounds__(256) void k_lscan(const LSeg *__restrict__ lsegs, const uint2 *__restrict__ segtiles,
                                                uint32_t *__restrict__ thist, uint32_t *__restrict__ nomove,
                                                uint2 *tiny, uint2 *med, LSeg *large_next, uint2 *groups, Counters *cnt)
@@ -511,7 +788,7 @@ __global__ __launch_bounds__(256) void k_lscan(const LSeg *__restrict__ lsegs, c
     const uint32_t d = threadIdx.x;
     uint32_t run = 0;
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
-        uint32_t v = thist[(size_t)t * 256 + d];
+        const uint32_t v = thist[(size_t)t * 256 + d];
         thist[(size_t)t * 256 + d] = run;
         run += v;
     }
@@ -573,7 +850,8 @@ __global__ __launch_bounds__(256) void k_groups(RoundArgs a, const uint2 *__rest
         const uint2 s = groups[g];
         const uint32_t b = find_block(a.boffs, a.nb, s.x);
         const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-        for (uint32_t e = l; e < s.y; e += 64) finish(a, boff, n, a.sa[s.x + e], s.x - boff, s.y, e == 0);
+        for (uint32_t e = l; e < s.y; e += 64)
+            finish(a, boff, n, a.sa[s.x + e], s.x + e, s.x - boff, s.y, e == 0);
     }
 }
 
@@ -584,29 +862,34 @@ __global__ void k_commit(const uint32_t *__restrict__ list, uint32_t cnt, const 
     if (i < cnt) dst[list[i]] = src[list[i]];
 }
 
-// ------------------------------------------------------------------------------ outputs
-// L[r] = data[(SA[r] + n - 1) mod n] (main.cpp:87); grid = (ceil(max_n / 4096), nblocks).
-__global__ __launch_bounds__(256) void k_lastcol(const uint8_t *__restrict__ data, const BlockInfo *__restrict__ blocks,
-                                                 const uint32_t *__restrict__ sa, uint8_t *__restrict__ L)
+__global__ void k_fill_u32(uint32_t *p, uint32_t v, uint32_t n)
 {
-    const BlockInfo bi = blocks[blockIdx.y];
-    const uint32_t j0 = blockIdx.x * 4096u;
-    if (j0 >= bi.n) return;
-    const uint32_t j1 = min(j0 + 4096u, bi.n);
-    for (uint32_t j = j0 + threadIdx.x; j < j1; j += 256) {
-        const uint32_t p = sa[bi.off + j];
-        L[bi.off + j] = data[bi.off + (p == 0 ? bi.n - 1 : p - 1)];
-    }
-}
-
-__global__ void k_primary(const BlockInfo *__restrict__ blocks, uint32_t nb, const uint32_t *__restrict__ rk,
-                          uint32_t *__restrict__ prim)
-{
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < nb) prim[b] = rk[blocks[b].off];  // rank of rotation 0 = #strictly smaller rotations
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
 }
 
 inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Host-side tiling of a segment list into <= kDTile pieces.
+template <class S, class T>
+void build_tiles(const std::vector<S> &segs, uint32_t tile, std::vector<T> &tiles, std::vector<uint2> &segtiles,
+                 uint32_t (*gstart)(const S &), uint32_t (*len)(const S &))
+{
+    tiles.clear();
+    segtiles.resize(segs.size());
+    for (uint32_t s = 0; s < segs.size(); ++s) {
+        segtiles[s].x = (uint32_t)tiles.size();
+        for (uint32_t o = 0; o < len(segs[s]); o += tile) {
+            T t;
+            t.seg = s;
+            t.start = gstart(segs[s]) + o;
+            t.len = std::min<uint32_t>(tile, len(segs[s]) - o);
+            t.pad = 0;
+            tiles.push_back(t);
+        }
+        segtiles[s].y = (uint32_t)tiles.size() - segtiles[s].x;
+    }
+}
 
 }  // namespace
 
@@ -616,181 +899,247 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     const uint64_t N = bt.total;
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
 
-    // ---- batch tables
-    std::vector<BlockInfo> hb(nb);
-    std::vector<uint32_t> hoffs(nb + 1), chunk_first(nb + 1), chunk_block;
+    // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8)
+    std::vector<uint32_t> hoffs(nb + 1);
+    for (uint32_t b = 0; b <= nb; ++b) hoffs[b] = (uint32_t)bt.offs[b];
+    std::vector<std::vector<GChunk>> lane(8);
     for (uint32_t b = 0; b < nb; ++b) {
-        hb[b].off = (uint32_t)bt.offs[b];
-        hb[b].n = (uint32_t)(bt.offs[b + 1] - bt.offs[b]);
-        hoffs[b] = hb[b].off;
-        chunk_first[b] = (uint32_t)chunk_block.size();
-        for (uint32_t k = 0; k < cdiv(hb[b].n, kHistChunk); ++k) chunk_block.push_back(b);
+        const uint32_t n = hoffs[b + 1] - hoffs[b];
+        for (uint32_t s = 0; s < n; s += kGChunk) lane[b & 7].push_back(GChunk{b, s, std::min(kGChunk, n - s), 0});
     }
-    hoffs[nb] = (uint32_t)N;
-    chunk_first[nb] = (uint32_t)chunk_block.size();
-    const uint32_t nchunks = (uint32_t)chunk_block.size();
+    size_t lmax = 0;
+    for (auto &l : lane) lmax = std::max(lmax, l.size());
+    std::vector<GChunk> chunks(lmax * 8, GChunk{0, 0, 0, 0});
+    std::vector<uint32_t> bchunks(nb, 0), bchunk0(nb, 0);
+    for (uint32_t x = 0; x < 8; ++x)
+        for (size_t k = 0; k < lane[x].size(); ++k) {
+            const GChunk &g = lane[x][k];
+            chunks[k * 8 + x] = g;
+            if (bchunks[g.block]++ == 0) bchunk0[g.block] = (uint32_t)(k * 8 + x);
+        }
+    const uint32_t nchunks = (uint32_t)chunks.size();
 
-    // blocks | boffs | chunk_first | chunk_block packed in one upload
-    const size_t tb_bytes = nb * sizeof(BlockInfo) + (nb + 1) * 4 * 2 + nchunks * 4;
-    uint8_t *d_tab = (uint8_t *)c->get(WS_BLOCKS, tb_bytes + 64);
+    const size_t tab_bytes = (nb + 1) * 4 + nb * 8 + nchunks * sizeof(GChunk);
+    uint8_t *d_tab = (uint8_t *)c->get(WS_BLOCKS, tab_bytes + 64);
     {
-        std::vector<uint8_t> h(tb_bytes);
+        std::vector<uint8_t> h(tab_bytes);
         size_t o = 0;
-        memcpy(&h[o], hb.data(), nb * sizeof(BlockInfo));
-        o += nb * sizeof(BlockInfo);
         memcpy(&h[o], hoffs.data(), (nb + 1) * 4);
         o += (nb + 1) * 4;
-        memcpy(&h[o], chunk_first.data(), (nb + 1) * 4);
-        o += (nb + 1) * 4;
-        memcpy(&h[o], chunk_block.data(), nchunks * 4);
-        BMH_HIP(hipMemcpyAsync(d_tab, h.data(), tb_bytes, hipMemcpyHostToDevice, c->stream));
-        c->sync();  // h goes out of scope
+        memcpy(&h[o], bchunks.data(), nb * 4);
+        o += nb * 4;
+        memcpy(&h[o], bchunk0.data(), nb * 4);
+        o += nb * 4;
+        memcpy(&h[o], chunks.data(), nchunks * sizeof(GChunk));
+        BMH_HIP(hipMemcpyAsync(d_tab, h.data(), tab_bytes, hipMemcpyHostToDevice, c->stream));
+        c->sync();
     }
-    const BlockInfo *d_blocks = (const BlockInfo *)d_tab;
-    const uint32_t *d_boffs = (const uint32_t *)(d_tab + nb * sizeof(BlockInfo));
-    const uint32_t *d_cfirst = d_boffs + (nb + 1);
-    const uint32_t *d_cblock = d_cfirst + (nb + 1);
+    const uint32_t *d_boffs = (const uint32_t *)d_tab;
+    const uint32_t *d_bchunks = d_boffs + (nb + 1);
+    const uint32_t *d_bchunk0 = d_bchunks + nb;
+    const GChunk *d_chunks = (const GChunk *)(d_bchunk0 + nb);
 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
-    uint32_t *rkA = (uint32_t *)c->get(WS_RKA, N * 4);
-    uint32_t *rkB = (uint32_t *)c->get(WS_RKB, N * 4);
-    uint32_t *key = (uint32_t *)c->get(WS_KEY, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
-    uint32_t *key2 = (uint32_t *)c->get(WS_KEY2, N * 4);
+    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kGBins * 4);
+    uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kGBins * 8);
     const size_t seg_cap = N / 2 + 2;
-    uint2 *seg_cur = (uint2 *)c->get(WS_SEG_CUR, seg_cap * 8);
-    uint2 *seg_nxt = (uint2 *)c->get(WS_SEG_NXT, seg_cap * 8);
-    uint2 *tiny = (uint2 *)c->get(WS_TINY, seg_cap * 8);
-    uint2 *med = (uint2 *)c->get(WS_MED, (N / (kTinyMax + 1) + 2) * 8);
-    const size_t lcap = N / (kMedMax + 1) + 2;
-    LSeg *large = (LSeg *)c->get(WS_LARGE, lcap * sizeof(LSeg));
-    LSeg *large2 = (LSeg *)c->get(WS_LARGE2, lcap * sizeof(LSeg));
-    uint2 *groups = (uint2 *)c->get(WS_GROUPS, (N + 2) * 8);
-    uint32_t *prefix = (uint32_t *)c->get(WS_PREFIX, seg_cap * 4);
-    uint32_t *partials = (uint32_t *)c->get(WS_SCAN_PART, (seg_cap / kScanItems + 2) * 4);
-    uint32_t *tiles = (uint32_t *)c->get(WS_TILES, seg_cap * 4);
-    uint32_t *resolved = (uint32_t *)c->get(WS_RESOLVED, N * 4);
+    // every list entry covers >= 2 positions, so N / 2 entries bound every list
+    Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, seg_cap * 16);
+    Seg4 *fin_nxt = (Seg4 *)c->get(WS_FIN_NXT, seg_cap * 16);
+    Seg4 *dgroups = (Seg4 *)c->get(WS_GROUPS, seg_cap * 16);
+    Seg4 *big = (Seg4 *)c->get(WS_LARGE, (N / kFinCap + 2) * 16);
+    Seg4 *big2 = (Seg4 *)c->get(WS_LARGE2, (N / kFinCap + 2) * 16);
+    uint32_t *bflag = (uint32_t *)c->get(WS_OFFS, nb * 4 + 64);
+    uint32_t *d_prim = (uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);
     Counters *d_cnt = (Counters *)c->get(WS_COUNTERS, sizeof(Counters) + 64);
-    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * 2 * kHalfBins * 4);
-    uint32_t *bstart = (uint32_t *)c->get(WS_BSTART, (size_t)nb * 65537 * 4);
     Counters *h_cnt = (Counters *)c->host_pinned(sizeof(Counters) + 4096);
-
     auto read_counters = [&]() {
         BMH_HIP(hipMemcpyAsync(h_cnt, d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         c->sync();
     };
 
-    // ---- bucket round: D = 2
+    DataArgs da;
+    da.data = d_in;
+    da.boffs = d_boffs;
+    da.nb = nb;
+    da.sa = sa;
+    da.L = d_L;
+    da.prim = d_prim;
+    da.bflag = bflag;
+    da.groups = dgroups;
+    da.cnt = d_cnt;
+
     BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
-    BMH_LAUNCH(c, "bwt_bucket_hist", k_bucket_hist, nchunks * 2, 1024, kHalfBins * 4, d_in, d_blocks, d_cblock,
-               d_cfirst, chist);
-    BMH_LAUNCH(c, "bwt_bucket_scan", k_bucket_scan, nb, 1024, 0, d_blocks, d_cfirst, chist, bstart, seg_cur, d_cnt);
-    BMH_LAUNCH(c, "bwt_bucket_scatter", k_bucket_scatter, nchunks * 2, 1024, kHalfBins * 4, d_in, d_blocks,
-               d_cblock, d_cfirst, chist, bstart, sa, rkA, rkB);
+    BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
+    BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
+
+    // ---- data phase
+    BMH_LAUNCH(c, "bwt_g12_hist", k_g12_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
+    BMH_LAUNCH(c, "bwt_g12_scan", k_g12_scan, nb, 1024, 0, d_boffs, nb, d_bchunks, d_bchunk0, chist, bk, big, d_cnt);
+    BMH_LAUNCH(c, "bwt_g12_scatter", k_g12_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk);
+    da.fin_next = fin_cur;
+    da.big_next = big2;
+    BMH_LAUNCH(c, "bwt_finish", k_finish, 8u * cdiv(nb, 8) * kGBins, kFinNT, 0, da, nullptr, bk, 1);
     read_counters();
-    uint32_t ncur = h_cnt->next;
-
-    uint64_t D = 2;
-    int round = 1;
-    std::vector<LSeg> hl;
-    std::vector<LTile> ht;
+    uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
+    Seg4 *big_cur = big, *big_nxt = big2;
+    std::vector<Seg4> hs;
+    std::vector<DTile> ht;
     std::vector<uint2> hst;
-    while (ncur > 0) {
-        RoundArgs a;
-        a.data = d_in;
-        a.boffs = d_boffs;
-        a.nb = nb;
-        a.sa = sa;
-        const bool odd = (round & 1) != 0;
-        a.rk_cur = odd ? rkB : rkA;  // round 1 reads nothing
-        a.rk_nxt = odd ? rkA : rkB;
-        a.rkA = rkA;
-        a.rkB = rkB;
-        a.D = (uint32_t)std::min<uint64_t>(D, 0xffffffffull);
-        a.newD = round == 1 ? 6 : 2 * D;
-        a.round1 = round == 1;
-        a.next = seg_nxt;
-        a.resolved = resolved;
-        a.cnt = d_cnt;
-
-        BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
-        BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt);
-        read_counters();
-
-        // ---- large segments: MSD radix passes until every piece is tiny/medium/group
-        uint32_t nl = h_cnt->large;
-        LSeg *lcur = large, *lnxt = large2;
-        while (nl > 0) {
-            hl.resize(nl);
-            BMH_HIP(hipMemcpyAsync(hl.data(), lcur, nl * sizeof(LSeg), hipMemcpyDeviceToHost, c->stream));
+    while (nfin > 0 || nbig > 0) {
+        BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 8, c->stream));  // fin_next, big_next
+        // finish segments first (they write fin_next -> other buffer)
+        if (nfin > 0) {
+            da.fin_next = fin_nxt;
+            da.big_next = big_nxt;
+            BMH_LAUNCH(c, "bwt_finish", k_finish, nfin, kFinNT, 0, da, fin_cur, bk, 0);
+        }
+        if (nbig > 0) {
+            hs.resize(nbig);
+            BMH_HIP(hipMemcpyAsync(hs.data(), big_cur, nbig * sizeof(Seg4), hipMemcpyDeviceToHost, c->stream));
             c->sync();
-            ht.clear();
-            hst.resize(nl);
-            for (uint32_t s = 0; s < nl; ++s) {
-                hst[s].x = (uint32_t)ht.size();
-                for (uint32_t o = 0; o < hl[s].len; o += kLargeTile) {
-                    LTile t;
-                    t.seg = s;
-                    t.start = hl[s].gstart + o;
-                    t.len = std::min<uint32_t>(kLargeTile, hl[s].len - o);
-                    t.pad = 0;
-                    ht.push_back(t);
-                }
-                hst[s].y = (uint32_t)ht.size() - hst[s].x;
-            }
+            build_tiles<Seg4, DTile>(hs, kDTile, ht, hst, [](const Seg4 &s) { return s.x; },
+                                     [](const Seg4 &s) { return s.y; });
             const uint32_t ntl = (uint32_t)ht.size();
-            uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(LTile) + nl * 8 + nl * 4 + 64);
-            LTile *d_tiles = (LTile *)d_lt;
-            uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(LTile));
-            uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(LTile) + nl * 8);
-            BMH_HIP(hipMemcpyAsync(d_tiles, ht.data(), ntl * sizeof(LTile), hipMemcpyHostToDevice, c->stream));
-            BMH_HIP(hipMemcpyAsync(d_segtiles, hst.data(), nl * 8, hipMemcpyHostToDevice, c->stream));
+            uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(DTile) + nbig * 8 + nbig * 4 + 64);
+            DTile *d_tiles = (DTile *)d_lt;
+            uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(DTile));
+            uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(DTile) + nbig * 8);
+            BMH_HIP(hipMemcpyAsync(d_tiles, ht.data(), ntl * sizeof(DTile), hipMemcpyHostToDevice, c->stream));
+            BMH_HIP(hipMemcpyAsync(d_segtiles, hst.data(), nbig * 8, hipMemcpyHostToDevice, c->stream));
             uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
-            BMH_HIP(hipMemsetAsync(&d_cnt->large_next, 0, 4, c->stream));
-            BMH_LAUNCH(c, "bwt_lhist", k_lhist, ntl, 256, 0, a, lcur, d_tiles, key, thist);
-            BMH_LAUNCH(c, "bwt_lscan", k_lscan, nl, 256, 0, lcur, d_segtiles, thist, d_nomove, tiny, med, lnxt,
-                       groups, d_cnt);
-            BMH_LAUNCH(c, "bwt_lscatter", k_lscatter, ntl, 256, 0, lcur, d_tiles, d_nomove, thist, sa, key, sa2,
-                       key2);
-            BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, ntl, 256, 0, d_tiles, d_nomove, sa, key, sa2, key2);
-            read_counters();
-            nl = h_cnt->large_next;
-            std::swap(lcur, lnxt);
+            uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
+            da.fin_next = fin_nxt;
+            da.big_next = big_nxt;
+            BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, thist);
+            BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, thist, stot, d_nomove);
+            BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, d_nomove, thist, stot, sa2);
+            BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
         }
-
-        // ---- tiny segments: pack into tiles, rank by counting
-        const uint32_t ntiny = h_cnt->tiny;
-        if (ntiny > 0) {
-            const uint32_t nparts = cdiv(ntiny, kScanItems);
-            BMH_LAUNCH(c, "bwt_scan_reduce", k_scan_reduce, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials);
-            BMH_LAUNCH(c, "bwt_scan_partials", k_scan_partials, 1, 1024, 0, partials, nparts);
-            BMH_LAUNCH(c, "bwt_scan_down", k_scan_down, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials, prefix);
-            BMH_LAUNCH(c, "bwt_tile_heads", k_tile_heads, cdiv(ntiny, 256), 256, 0, prefix, ntiny, tiles, d_cnt);
-            read_counters();
-            BMH_LAUNCH(c, "bwt_tiny", k_tiny, h_cnt->tiles, 256, 0, a, tiny, ntiny, prefix, tiles);
-        }
-        if (h_cnt->med > 0) BMH_LAUNCH(c, "bwt_medium", k_medium, h_cnt->med, kMedNT, 0, a, med);
-        if (h_cnt->groups > 0)
-            BMH_LAUNCH(c, "bwt_groups", k_groups, std::min<uint32_t>(cdiv(h_cnt->groups, 4), 65536), 256, 0, a,
-                       groups, h_cnt->groups);
         read_counters();
-        if (round > 1 && h_cnt->resolved > 0)
-            BMH_LAUNCH(c, "bwt_commit", k_commit, cdiv(h_cnt->resolved, 256), 256, 0, resolved, h_cnt->resolved,
-                       a.rk_nxt, (uint32_t *)a.rk_cur);
-        ncur = h_cnt->next;
-        std::swap(seg_cur, seg_nxt);
-        D = a.newD;
-        ++round;
+        nfin = h_cnt->fin_next;
+        nbig = h_cnt->big_next;
+        std::swap(fin_cur, fin_nxt);
+        std::swap(big_cur, big_nxt);
     }
 
-    // ---- outputs
-    BMH_LAUNCH(c, "bwt_lastcol", k_lastcol, dim3(cdiv(bt.max_n, 4096), nb), 256, 0, d_in, d_blocks, sa, d_L);
-    uint32_t *d_prim = (uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);
-    BMH_LAUNCH(c, "bwt_primary", k_primary, cdiv(nb, 256), 256, 0, d_blocks, nb, rkA, d_prim);
+    // ---- doubling phase, only if some block still holds tied groups
+    const uint32_t ngroups = h_cnt->dgroups;
+    if (ngroups > 0) {
+        uint32_t *rkA = (uint32_t *)c->get(WS_RKA, N * 4);
+        uint32_t *rkB = (uint32_t *)c->get(WS_RKB, N * 4);
+        uint32_t *key = (uint32_t *)c->get(WS_KEY, N * 4);
+        uint32_t *key2 = (uint32_t *)c->get(WS_KEY2, N * 4);
+        uint2 *seg_cur = (uint2 *)c->get(WS_DSEG_CUR, seg_cap * 8);
+        uint2 *seg_nxt = (uint2 *)c->get(WS_DSEG_NXT, seg_cap * 8);
+        uint2 *tiny = (uint2 *)c->get(WS_TINY, seg_cap * 8);
+        uint2 *med = (uint2 *)c->get(WS_MED, (N / (kTinyMax + 1) + 2) * 8);
+        const size_t lcap = N / (kMedMax + 1) + 2;
+        LSeg *large = (LSeg *)c->get(WS_DLARGE, lcap * sizeof(LSeg));
+        LSeg *large2 = (LSeg *)c->get(WS_DLARGE2, lcap * sizeof(LSeg));
+        uint2 *groups = (uint2 *)c->get(WS_DGROUPS, (N + 2) * 8);
+        uint32_t *prefix = (uint32_t *)c->get(WS_PREFIX, seg_cap * 4);
+        uint32_t *partials = (uint32_t *)c->get(WS_SCAN_PART, (seg_cap / kScanItems + 2) * 4);
+        uint32_t *tiles = (uint32_t *)c->get(WS_TILES, seg_cap * 4);
+        uint32_t *resolved = (uint32_t *)c->get(WS_RESOLVED, N * 4);
+
+        BMH_LAUNCH(c, "bwt_rank_fill", k_rank_fill, dim3(cdiv(bt.max_n, 4096), nb), 256, 0, d_boffs, bflag, sa, rkA,
+                   rkB);
+        BMH_HIP(hipMemsetAsync(&d_cnt->next, 0, 4, c->stream));
+        BMH_HIP(hipMemsetAsync(&d_cnt->dmin_bits, 0xff, 4, c->stream));
+        BMH_LAUNCH(c, "bwt_group_fill", k_group_fill, std::min<uint32_t>(cdiv(ngroups, 4), 65536), 256, 0, da, dgroups,
+                   ngroups, rkA, rkB, seg_cur, d_cnt);
+        read_counters();
+        uint32_t ncur = h_cnt->next;
+        uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
+        int round = 0;
+        std::vector<LSeg> hl;
+        std::vector<LTile> hlt;
+        std::vector<uint2> hlst;
+        while (ncur > 0) {
+            if (D == 0) fail(BMH_EHIP, "bwt: internal error (zero doubling depth)");
+            RoundArgs a;
+            a.data = d_in;
+            a.boffs = d_boffs;
+            a.nb = nb;
+            a.sa = sa;
+            a.L = d_L;
+            a.prim = d_prim;
+            const bool odd = (round & 1) != 0;
+            a.rk_cur = odd ? rkB : rkA;
+            a.rk_nxt = odd ? rkA : rkB;
+            a.D = (uint32_t)std::min<uint64_t>(D, 0xffffffffull);
+            a.newD = 2 * D;
+            a.next = seg_nxt;
+            a.resolved = resolved;
+            a.cnt = d_cnt;
+
+            BMH_HIP(hipMemsetAsync(d_cnt, 0, 8 * 4, c->stream));  // the 8 doubling-phase counters
+            BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt);
+            read_counters();
+
+            uint32_t nl = h_cnt->large;
+            LSeg *lcur = large, *lnxt = large2;
+            while (nl > 0) {
+                hl.resize(nl);
+                BMH_HIP(hipMemcpyAsync(hl.data(), lcur, nl * sizeof(LSeg), hipMemcpyDeviceToHost, c->stream));
+                c->sync();
+                build_tiles<LSeg, LTile>(hl, kDTile, hlt, hlst, [](const LSeg &s) { return s.gstart; },
+                                         [](const LSeg &s) { return s.len; });
+                const uint32_t ntl = (uint32_t)hlt.size();
+                uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(LTile) + nl * 8 + nl * 4 + 64);
+                LTile *d_tiles = (LTile *)d_lt;
+                uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(LTile));
+                uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(LTile) + nl * 8);
+                BMH_HIP(hipMemcpyAsync(d_tiles, hlt.data(), ntl * sizeof(LTile), hipMemcpyHostToDevice, c->stream));
+                BMH_HIP(hipMemcpyAsync(d_segtiles, hlst.data(), nl * 8, hipMemcpyHostToDevice, c->stream));
+                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
+                BMH_HIP(hipMemsetAsync(&d_cnt->large_next, 0, 4, c->stream));
+                BMH_LAUNCH(c, "bwt_lhist", k_lhist, ntl, 256, 0, a, lcur, d_tiles, key, thist);
+                BMH_LAUNCH(c, "bwt_lscan", k_lscan, nl, 256, 0, lcur, d_segtiles, thist, d_nomove, tiny, med, lnxt,
+                           groups, d_cnt);
+                BMH_LAUNCH(c, "bwt_lscatter", k_lscatter, ntl, 256, 0, lcur, d_tiles, d_nomove, thist, sa, key, sa2,
+                           key2);
+                BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, ntl, 256, 0, d_tiles, d_nomove, sa, key, sa2, key2);
+                read_counters();
+                nl = h_cnt->large_next;
+                std::swap(lcur, lnxt);
+            }
+
+            const uint32_t ntiny = h_cnt->tiny;
+            if (ntiny > 0) {
+                const uint32_t nparts = cdiv(ntiny, kScanItems);
+                BMH_LAUNCH(c, "bwt_scan_reduce", k_scan_reduce, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials);
+                BMH_LAUNCH(c, "bwt_scan_partials", k_scan_partials, 1, 1024, 0, partials, nparts);
+                BMH_LAUNCH(c, "bwt_scan_down", k_scan_down, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials, prefix);
+                BMH_LAUNCH(c, "bwt_tile_heads", k_tile_heads, cdiv(ntiny, 256), 256, 0, prefix, ntiny, tiles, d_cnt);
+                read_counters();
+                BMH_LAUNCH(c, "bwt_tiny", k_tiny, h_cnt->tiles, 256, 0, a, tiny, ntiny, prefix, tiles);
+            }
+            if (h_cnt->med > 0) BMH_LAUNCH(c, "bwt_medium", k_medium, h_cnt->med, kMedNT, 0, a, med);
+            if (h_cnt->groups > 0)
+                BMH_LAUNCH(c, "bwt_groups", k_groups, std::min<uint32_t>(cdiv(h_cnt->groups, 4), 65536), 256, 0, a,
+                           groups, h_cnt->groups);
+            read_counters();
+            if (h_cnt->resolved > 0)
+                BMH_LAUNCH(c, "bwt_commit", k_commit, cdiv(h_cnt->resolved, 256), 256, 0, resolved, h_cnt->resolved,
+                           a.rk_nxt, (uint32_t *)a.rk_cur);
+            ncur = h_cnt->next;
+            std::swap(seg_cur, seg_nxt);
+            D = a.newD;
+            ++round;
+        }
+    }
+
+    // ---- primary indices
     uint32_t *h_prim = (uint32_t *)c->host_pinned(nb * 4 + 4096);
     BMH_HIP(hipMemcpyAsync(h_prim, d_prim, nb * 4, hipMemcpyDeviceToHost, c->stream));
     c->sync();
-    for (uint32_t b = 0; b < nb; ++b) h_primary[b] = h_prim[b];
+    for (uint32_t b = 0; b < nb; ++b) {
+        if (h_prim[b] == 0xffffffffu) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
+        h_primary[b] = h_prim[b];
+    }
 }
 
 }  // namespace bmh

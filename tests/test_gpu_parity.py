@@ -45,6 +45,34 @@ def test_bwt_matches_oracle(ctx, oracle, name):
     assert prim == oprim
 
 
+def test_bwt_tiny_blocks_batched(ctx, oracle):
+    """n = 1..40 over 1-3 symbol alphabets, all in one batch: periodic / identical rotations."""
+    rng = np.random.default_rng(11)
+    blocks = []
+    for n in range(1, 41):
+        for alpha in (1, 2, 3):
+            blocks.append(rng.integers(0, alpha, n, dtype=np.uint8).tobytes())
+        blocks.append((b"ab" * n)[:n])
+    arrs = [np.frombuffer(b, np.uint8) for b in blocks]
+    offs = np.zeros(len(arrs) + 1, np.uint64)
+    offs[1:] = np.cumsum([a.size for a in arrs])
+    d_in, d_L = ctx.alloc(int(offs[-1])), ctx.alloc(int(offs[-1]))
+    d_in.upload(np.concatenate(arrs))
+    prim = ctx.bwt_dev(d_in, offs, d_L)
+    L = d_L.download()
+    for i, b in enumerate(blocks):
+        op, oL = oracle.bwt(b)
+        assert (int(prim[i]), L[int(offs[i]):int(offs[i + 1])].tobytes()) == (op, oL), (i, b)
+
+
+def test_bwt_big_degenerate(ctx, oracle):
+    """4 MiB of zeros and a 4 MiB period-3 block: MSD no-move passes, then rank doubling."""
+    for data in (bytes(1 << 22), (b"xyz" * ((1 << 22) // 3 + 1))[: 1 << 22]):
+        prim, L = bmh.bwt(data, ctx)
+        op, oL = oracle.bwt(data)
+        assert prim == op and L == oL
+
+
 def test_bwt_batch_mixed_blocks(ctx, oracle):
     blocks = [EDGE[k] for k in sorted(EDGE)]
     arrs = [np.frombuffer(b, np.uint8) for b in blocks]
