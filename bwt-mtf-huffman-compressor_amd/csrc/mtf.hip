@@ -3,15 +3,23 @@
 //
 // Replaces move_to_front() (reference main.cpp:93-112: find_if + std::rotate over a 256-byte
 // alphabet initialised 0..255) and the two O(n) scans at the top of huffman()
-// (main.cpp:231-244). MTF is sequential per block, so each block is cut into chunks:
-//   1. recency  : per chunk, its distinct symbols ordered by last occurrence (most recent
-//                 first) — LDS atomicMax of positions, then a rank count.
-//   2. compose  : per block, one wave walks its chunks in order: state_{c+1} =
-//                 recency_c ++ (state_c minus recency_c); writes each chunk's start state.
-//   3. encode   : one wave per chunk runs MTF from its start state. The alphabet is held as
-//                 pos[s] (current index of symbol s), 4 symbols per lane in 4 VGPRs; a step
-//                 is readlane(pos[c]) + "pos += pos < pc" on all 256 entries + writelane 0.
-//                 Output bytes also feed per-wave LDS histograms / first-occurrence minima.
+// (main.cpp:231-244). MTF is sequential per block, so each block is cut into 4 KiB chunks:
+//   1. recency : per chunk, its distinct symbols ordered by last occurrence (most recent
+//                first): LDS atomicMax of positions, a bitset of last-occurrence positions,
+//                then a suffix popcount gives each symbol's rank.
+//   2. compose : per block, one wave walks its chunks in order: state_{c+1} =
+//                recency_c ++ (state_c minus recency_c); this is each chunk's start state.
+//   3. encode  : ONE LANE PER CHUNK. The alphabet is kept as time stamps, not as a list:
+//                tm[s] = slot of the last access of symbol s in a 512-slot window, and a slot
+//                bit is set iff it is some symbol's last access (always 256 marks). The MTF
+//                index of c is the number of marks above tm[c] (symbols used more recently),
+//                counted in two levels: whole superwords above (4 byte counters in a VGPR),
+//                words above inside c's superword (byte counters in LDS), bits above inside
+//                c's word (one popcount). An access clears one mark and sets the next slot —
+//                O(1) work instead of moving up to 255 list entries; the window is renumbered
+//                every 256 symbols. (tools/microbench/mtf_variants.hip: 4.6 ms per GiB vs
+//                28-40 ms for whole-wave list updates on MI355X.)
+//   4. hist    : freq + first occurrence of each MTF value per block (LDS atomics).
 #include "bmh_internal.h"
 #include "device_util.h"
 
@@ -21,28 +29,49 @@ namespace bmh {
 
 namespace {
 
+constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
+constexpr int kLanes = 256;           // lanes (chunks) per encode workgroup
+
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
 };
 
+// grid = chunks; 256 threads. R[c][0..d) = distinct symbols, most recent last occurrence first.
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                      uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
 {
     __shared__ int lastpos[256];
+    __shared__ uint32_t bset[kMtfChunk / 32];
+    __shared__ uint32_t s_tmp[8];
     const MChunk ch = chunks[blockIdx.x];
-    lastpos[threadIdx.x] = -1;
+    const uint32_t t = threadIdx.x;
+    lastpos[t] = -1;
+    if (t < kMtfChunk / 32) bset[t] = 0;
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < ch.len; i += 256) atomicMax(&lastpos[L[ch.start + i]], (int)i);
+    for (uint32_t i = t; i < ch.len; i += 256) atomicMax(&lastpos[L[ch.start + i]], (int)i);
     __syncthreads();
-    const int lp = lastpos[threadIdx.x];
-    uint32_t rank = 0;
-    for (int s = 0; s < 256; ++s) rank += lastpos[s] > lp;
+    const int lp = lastpos[t];
+    if (lp >= 0) atomicOr(&bset[lp >> 5], 1u << (lp & 31));
     const int d = __syncthreads_count(lp >= 0);
-    if (lp >= 0) R[(size_t)blockIdx.x * 256 + rank] = (uint8_t)threadIdx.x;
-    if (threadIdx.x == 0) dcount[blockIdx.x] = (uint32_t)d;
+    // thread t owns positions [16t, 16t+16); ranks count set bits at higher positions
+    const uint32_t v = (bset[t >> 1] >> (16 * (t & 1))) & 0xffffu;
+    const uint32_t cnt = __builtin_popcount(v);
+    const uint32_t rt = 255 - t;  // reversed order -> exclusive sum = bits at higher positions
+    uint32_t off = 0;
+    {
+        // exclusive prefix over reversed thread order
+        uint32_t total;
+        const uint32_t ex_rev = block_excl_sum<256>(cnt, s_tmp, &total);  // sum over threads < t
+        off = total - ex_rev - cnt;                                         // sum over threads > t
+        (void)rt;
+    }
+    uint8_t *Rc = R + (size_t)blockIdx.x * 256;
+    for (int b = 15; b >= 0; --b)
+        if (v & (1u << b)) Rc[off++] = L[ch.start + 16 * t + b];
+    if (t == 0) dcount[blockIdx.x] = (uint32_t)d;
 }
 
-// grid = nblocks, one wave each.
+// grid = nblocks, one wave each: sequential composition of the chunk recency lists.
 __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__ chunk_first,
                                                     const uint8_t *__restrict__ R, const uint32_t *__restrict__ dcount,
                                                     uint32_t *__restrict__ S)
@@ -75,87 +104,95 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__
     }
 }
 
-#define MTF_STEP(SYM, OUTV)                                                                 \
-    do {                                                                                    \
-        const uint32_t c_ = (SYM);                                                          \
-        const uint32_t ln_ = c_ >> 2;                                                       \
-        uint32_t pc_;                                                                       \
-        switch (c_ & 3u) {                                                                  \
-        case 0: pc_ = __builtin_amdgcn_readlane(p0, ln_); break;                            \
-        case 1: pc_ = __builtin_amdgcn_readlane(p1, ln_); break;                            \
-        case 2: pc_ = __builtin_amdgcn_readlane(p2, ln_); break;                            \
-        default: pc_ = __builtin_amdgcn_readlane(p3, ln_); break;                           \
-        }                                                                                   \
-        p0 += p0 < pc_ ? 1u : 0u;                                                           \
-        p1 += p1 < pc_ ? 1u : 0u;                                                           \
-        p2 += p2 < pc_ ? 1u : 0u;                                                           \
-        p3 += p3 < pc_ ? 1u : 0u;                                                           \
-        switch (c_ & 3u) {                                                                  \
-        case 0: p0 = writelane(0, ln_, p0); break;                         \
-        case 1: p1 = writelane(0, ln_, p1); break;                         \
-        case 2: p2 = writelane(0, ln_, p2); break;                         \
-        default: p3 = writelane(0, ln_, p3); break;                        \
-        }                                                                                   \
-        OUTV = pc_;                                                                         \
-    } while (0)
-
-// grid = chunks, one wave each.
-__global__ __launch_bounds__(64) void k_mtf_encode(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
-                                                   const uint32_t *__restrict__ S, uint8_t *__restrict__ out,
-                                                   uint32_t *__restrict__ freq, uint32_t *__restrict__ first)
+// Marks above slot t: bits above in t's word + words above in t's superword + superwords above.
+__device__ __forceinline__ uint32_t marks_above(uint32_t t, uint32_t S, const uint32_t *bits, const uint32_t *cnt,
+                                                uint32_t l)
 {
-    __shared__ uint8_t s_pos[256];
-    __shared__ uint32_t s_hist[256], s_first[256];
-    const MChunk ch = chunks[blockIdx.x];
+    const uint32_t ws = t >> 5, sb = t & 31u, wq = ws >> 2, wr = ws & 3u;
+    const uint32_t bw = bits[ws * kLanes + l];
+    const uint32_t cw = cnt[wq * kLanes + l];
+    uint32_t r = __builtin_popcount((bw >> sb) >> 1);
+    r = __builtin_amdgcn_sad_u8(cw & (0xFFFFFF00u << (8 * wr)), 0u, r);
+    r = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << (8 * wq)), 0u, r);
+    return r;
+}
+
+__device__ __forceinline__ void window_reset(uint32_t *bits, uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t &now)
+{
+    for (uint32_t w = 0; w < 16; ++w) bits[w * kLanes + l] = w < 8 ? 0xffffffffu : 0u;
+    for (uint32_t q = 0; q < 4; ++q) cnt[q * kLanes + l] = q < 2 ? 0x20202020u : 0u;
+    S = 0x00008080u;
+    now = 256;
+}
+
+// grid = ceil(chunks / 256); one lane per chunk.
+__global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
+                                                       uint32_t nch, const uint32_t *__restrict__ Sst,
+                                                       uint8_t *__restrict__ out)
+{
+    __shared__ uint16_t tm[256 * kLanes];
+    __shared__ uint32_t bits[16 * kLanes];
+    __shared__ uint32_t cnt[4 * kLanes];
     const uint32_t l = threadIdx.x;
-    {
-        const uint32_t w = S[(size_t)blockIdx.x * 64 + l];
-        for (int k = 0; k < 4; ++k) s_pos[(w >> (8 * k)) & 255u] = (uint8_t)(4 * l + k);
-        for (int k = 0; k < 4; ++k) {
-            s_hist[4 * l + k] = 0;
-            s_first[4 * l + k] = 0xffffffffu;
+    const uint32_t g = blockIdx.x * kLanes + l;
+    if (g >= nch) return;  // no workgroup barriers below: lanes are independent
+    const MChunk ch = chunks[g];
+    const uint32_t *st = Sst + (size_t)g * 64;
+    for (uint32_t k4 = 0; k4 < 64; ++k4) {
+        const uint32_t w = st[k4];
+        for (uint32_t j = 0; j < 4; ++j) tm[((w >> (8 * j)) & 255u) * kLanes + l] = (uint16_t)(255 - (4 * k4 + j));
+    }
+    uint32_t S, now;
+    window_reset(bits, cnt, l, S, now);
+    const uint8_t *src = L + ch.start;
+    uint8_t *dst = out + ch.start;
+    for (uint32_t i = 0; i < ch.len; ++i) {
+        const uint32_t c = src[i];
+        const uint32_t t = tm[c * kLanes + l];
+        dst[i] = (uint8_t)marks_above(t, S, bits, cnt, l);
+        const uint32_t ws = t >> 5, wq = ws >> 2;
+        tm[c * kLanes + l] = (uint16_t)now;
+        atomicXor(&bits[ws * kLanes + l], 1u << (t & 31u));
+        atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
+        S -= 1u << (8 * wq);
+        const uint32_t wn = now >> 5;
+        atomicOr(&bits[wn * kLanes + l], 1u << (now & 31u));
+        atomicAdd(&cnt[(wn >> 2) * kLanes + l], 1u << (8 * (wn & 3u)));
+        S += 1u << (8 * (wn >> 2));
+        if (++now == 512) {  // renumber: slot of each symbol -> 255 - marks above it
+            for (uint32_t s = 0; s < 256; ++s) {
+                const uint32_t ts = tm[s * kLanes + l];
+                tm[s * kLanes + l] = (uint16_t)(255 - marks_above(ts, S, bits, cnt, l));
+            }
+            window_reset(bits, cnt, l, S, now);
         }
     }
+}
+
+struct HChunk {
+    uint32_t block, start, len, rel;
+};
+
+// freq + first occurrence of each MTF value, per block (huffman() main.cpp:231-244).
+__global__ __launch_bounds__(256) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
+                                                  uint32_t *__restrict__ freq, uint32_t *__restrict__ first)
+{
+    __shared__ uint32_t h[4][256], f[256];
+    const HChunk ch = chunks[blockIdx.x];
+    const uint32_t t = threadIdx.x, w = t >> 6;
+    for (int k = 0; k < 4; ++k) h[k][t] = 0;
+    f[t] = 0xffffffffu;
     __syncthreads();
-    uint32_t p0 = s_pos[4 * l + 0], p1 = s_pos[4 * l + 1], p2 = s_pos[4 * l + 2], p3 = s_pos[4 * l + 3];
-    for (uint32_t base = 0; base < ch.len; base += 256) {
-        const uint32_t nb = min(256u, ch.len - base);
-        const uint32_t i0 = base + 4 * l;
-        uint32_t w = 0;
-        for (int k = 0; k < 4; ++k)
-            if (i0 + k < ch.len) w |= (uint32_t)L[ch.start + i0 + k] << (8 * k);
-        uint32_t outw = 0;
-        const uint32_t nq = (nb + 3) >> 2;
-        for (uint32_t q = 0; q < nq; ++q) {
-            const uint32_t wq = __builtin_amdgcn_readlane(w, q);
-            uint32_t o0, o1 = 0, o2 = 0, o3 = 0;
-            MTF_STEP(wq & 255u, o0);
-            if (4 * q + 3 < nb) {
-                MTF_STEP((wq >> 8) & 255u, o1);
-                MTF_STEP((wq >> 16) & 255u, o2);
-                MTF_STEP(wq >> 24, o3);
-            } else {
-                if (4 * q + 1 < nb) MTF_STEP((wq >> 8) & 255u, o1);
-                if (4 * q + 2 < nb) MTF_STEP((wq >> 16) & 255u, o2);
-            }
-            outw = writelane(o0 | (o1 << 8) | (o2 << 16) | (o3 << 24), q, outw);
-        }
-        for (int k = 0; k < 4; ++k) {
-            if (i0 + k < ch.len) {
-                const uint32_t v = (outw >> (8 * k)) & 255u;
-                out[ch.start + i0 + k] = (uint8_t)v;
-                atomicAdd(&s_hist[v], 1u);
-                atomicMin(&s_first[v], ch.rel + i0 + k);
-            }
-        }
+    for (uint32_t i = t; i < ch.len; i += 256) {
+        const uint32_t v = in[ch.start + i];
+        atomicAdd(&h[w][v], 1u);
+        if (ch.rel + i < f[v]) atomicMin(&f[v], ch.rel + i);  // racy read only skips non-minima
     }
     __syncthreads();
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t s = 4 * l + k;
-        if (s_hist[s]) {
-            atomicAdd(&freq[(size_t)ch.block * 256 + s], s_hist[s]);
-            atomicMin(&first[(size_t)ch.block * 256 + s], s_first[s]);
-        }
+    const uint32_t tot = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+    if (tot) {
+        atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
+        atomicMin(&first[(size_t)ch.block * 256 + t], f[t]);
     }
 }
 
@@ -170,30 +207,32 @@ __global__ void k_fill_u32(uint32_t *p, uint32_t v, size_t n)
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32, uint32_t *h_first32)
 {
     const uint32_t nb = bt.nblocks;
-    // chunk length: aim for >= ~8K waves on a big batch, 4K..64K symbols per chunk
-    uint64_t target = bt.total / 8192;
-    uint32_t ch = 4096;
-    while (ch < target && ch < 65536) ch <<= 1;
     std::vector<MChunk> hc;
+    std::vector<HChunk> hh;
     std::vector<uint32_t> cfirst(nb + 1);
     for (uint32_t b = 0; b < nb; ++b) {
         cfirst[b] = (uint32_t)hc.size();
         const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
-        for (uint64_t s = 0; s < n; s += ch) {
+        for (uint64_t s = 0; s < n; s += kMtfChunk) {
             MChunk m;
             m.block = b;
             m.start = (uint32_t)(o + s);
-            m.len = (uint32_t)std::min<uint64_t>(ch, n - s);
+            m.len = (uint32_t)std::min<uint64_t>(kMtfChunk, n - s);
             m.rel = (uint32_t)s;
             hc.push_back(m);
         }
+        for (uint64_t s = 0; s < n; s += 65536)
+            hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
     }
     cfirst[nb] = (uint32_t)hc.size();
-    const uint32_t nch = (uint32_t)hc.size();
-    uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, nch * sizeof(MChunk) + (nb + 1) * 4 + 64);
+    const uint32_t nch = (uint32_t)hc.size(), nhh = (uint32_t)hh.size();
+    const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + (nb + 1) * 4;
+    uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + 64);
     MChunk *d_chunks = (MChunk *)d_tab;
-    uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk));
+    HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
+    uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));
     BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(MChunk), hipMemcpyHostToDevice, c->stream));
+    BMH_HIP(hipMemcpyAsync(d_hh, hh.data(), nhh * sizeof(HChunk), hipMemcpyHostToDevice, c->stream));
     BMH_HIP(hipMemcpyAsync(d_cfirst, cfirst.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
@@ -205,7 +244,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                (size_t)nb * 256);
     BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, nch, 256, 0, d_L, d_chunks, d_R, d_dcount);
     BMH_LAUNCH(c, "mtf_compose", k_mtf_compose, nb, 64, 0, d_cfirst, d_R, d_dcount, d_S);
-    BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, nch, 64, 0, d_L, d_chunks, d_S, d_mtf, d_freq, d_first);
+    BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
+    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_freq, d_first);
     if (h_freq32) BMH_HIP(hipMemcpyAsync(h_freq32, d_freq, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
     if (h_first32) BMH_HIP(hipMemcpyAsync(h_first32, d_first, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
     c->sync();
