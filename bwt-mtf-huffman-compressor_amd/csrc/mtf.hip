@@ -125,7 +125,29 @@ __device__ __forceinline__ void window_reset(uint32_t *bits, uint32_t *cnt, uint
     now = 256;
 }
 
-// grid = ceil(chunks / 256); one lane per chunk.
+// One MTF step for symbol c on this lane's state (slot `now`); returns the MTF index.
+__device__ __forceinline__ uint32_t mtf_step(uint32_t c, uint16_t *tm, uint32_t *bits, uint32_t *cnt, uint32_t l,
+                                             uint32_t &S, uint32_t now)
+{
+    const uint32_t t = tm[c * kLanes + l];
+    const uint32_t idx = marks_above(t, S, bits, cnt, l);
+    const uint32_t ws = t >> 5, wq = ws >> 2;
+    tm[c * kLanes + l] = (uint16_t)now;
+    atomicXor(&bits[ws * kLanes + l], 1u << (t & 31u));
+    atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
+    S -= 1u << (8 * wq);
+    const uint32_t wn = now >> 5;
+    atomicOr(&bits[wn * kLanes + l], 1u << (now & 31u));
+    atomicAdd(&cnt[(wn >> 2) * kLanes + l], 1u << (8 * (wn & 3u)));
+    S += 1u << (8 * (wn >> 2));
+    return idx;
+}
+
+// grid = ceil(chunks / 256); one lane per chunk. Chunks start 16-byte aligned except a block's
+// (<= 15-byte) first chunk; all lanes step through 16-symbol groups in lockstep so that the
+// slot counter `now` (and the renumbering every 256 slots) stays wave-uniform; a lane whose
+// group holds fewer than 16 of its symbols predicates the missing steps off (their slots stay
+// unmarked, which is harmless: slots only order accesses).
 __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                        uint32_t nch, const uint32_t *__restrict__ Sst,
                                                        uint8_t *__restrict__ out)
@@ -135,36 +157,56 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
     __shared__ uint32_t cnt[4 * kLanes];
     const uint32_t l = threadIdx.x;
     const uint32_t g = blockIdx.x * kLanes + l;
-    if (g >= nch) return;  // no workgroup barriers below: lanes are independent
-    const MChunk ch = chunks[g];
-    const uint32_t *st = Sst + (size_t)g * 64;
-    for (uint32_t k4 = 0; k4 < 64; ++k4) {
-        const uint32_t w = st[k4];
-        for (uint32_t j = 0; j < 4; ++j) tm[((w >> (8 * j)) & 255u) * kLanes + l] = (uint16_t)(255 - (4 * k4 + j));
+    const bool live = g < nch;
+    const MChunk ch = live ? chunks[g] : MChunk{0, 0, 0, 0};
+    if (live) {
+        const uint32_t *st = Sst + (size_t)g * 64;
+        for (uint32_t k4 = 0; k4 < 64; ++k4) {
+            const uint32_t w = st[k4];
+            for (uint32_t j = 0; j < 4; ++j) tm[((w >> (8 * j)) & 255u) * kLanes + l] = (uint16_t)(255 - (4 * k4 + j));
+        }
     }
     uint32_t S, now;
     window_reset(bits, cnt, l, S, now);
-    const uint8_t *src = L + ch.start;
-    uint8_t *dst = out + ch.start;
-    for (uint32_t i = 0; i < ch.len; ++i) {
-        const uint32_t c = src[i];
-        const uint32_t t = tm[c * kLanes + l];
-        dst[i] = (uint8_t)marks_above(t, S, bits, cnt, l);
-        const uint32_t ws = t >> 5, wq = ws >> 2;
-        tm[c * kLanes + l] = (uint16_t)now;
-        atomicXor(&bits[ws * kLanes + l], 1u << (t & 31u));
-        atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
-        S -= 1u << (8 * wq);
-        const uint32_t wn = now >> 5;
-        atomicOr(&bits[wn * kLanes + l], 1u << (now & 31u));
-        atomicAdd(&cnt[(wn >> 2) * kLanes + l], 1u << (8 * (wn & 3u)));
-        S += 1u << (8 * (wn >> 2));
-        if (++now == 512) {  // renumber: slot of each symbol -> 255 - marks above it
-            for (uint32_t s = 0; s < 256; ++s) {
-                const uint32_t ts = tm[s * kLanes + l];
-                tm[s * kLanes + l] = (uint16_t)(255 - marks_above(ts, S, bits, cnt, l));
+    const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
+    const uint32_t ngroups = live ? (((end + 15u) & ~15u) - base) >> 4 : 0u;
+    for (uint32_t grp = 0; __builtin_amdgcn_ballot_w64(grp < ngroups) != 0; ++grp) {
+        const uint32_t a = base + 16 * grp;
+        const bool full = grp < ngroups && a >= ch.start && a + 16 <= end;
+        uint4 in4 = make_uint4(0, 0, 0, 0);
+        if (full) {
+            in4 = *(const uint4 *)(L + a);
+        } else if (grp < ngroups) {
+            uint32_t *iw = &in4.x;
+            for (uint32_t k = 0; k < 16; ++k)
+                if (a + k >= ch.start && a + k < end) iw[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
+        }
+        uint4 o4;
+        uint32_t *o = &o4.x;
+        const uint32_t *iw = &in4.x;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            uint32_t ow = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t pos = a + 4 * w + k;
+                if (grp < ngroups && pos >= ch.start && pos < end)
+                    ow |= mtf_step((iw[w] >> (8 * k)) & 255u, tm, bits, cnt, l, S, now) << (8 * k);
+                if (++now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
+                    for (uint32_t s = 0; s < 256; ++s) {
+                        const uint32_t ts = tm[s * kLanes + l];
+                        tm[s * kLanes + l] = (uint16_t)(255 - marks_above(ts, S, bits, cnt, l));
+                    }
+                    window_reset(bits, cnt, l, S, now);
+                }
             }
-            window_reset(bits, cnt, l, S, now);
+            o[w] = ow;
+        }
+        if (full) {
+            *(uint4 *)(out + a) = o4;
+        } else if (grp < ngroups) {
+            for (uint32_t k = 0; k < 16; ++k)
+                if (a + k >= ch.start && a + k < end) out[a + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
         }
     }
 }
@@ -213,13 +255,19 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     for (uint32_t b = 0; b < nb; ++b) {
         cfirst[b] = (uint32_t)hc.size();
         const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
-        for (uint64_t s = 0; s < n; s += kMtfChunk) {
+        // chunk boundaries on 16-byte multiples of the batch (a block's first chunk takes the
+        // unaligned prefix) so the encode kernel moves 16 symbols per vector load / store
+        for (uint64_t s = 0; s < n;) {
+            const uint64_t gpos = o + s;
+            const uint64_t lim = (gpos & 15u) ? ((gpos + 15) & ~15ull) : gpos + kMtfChunk;
+            const uint64_t e = std::min<uint64_t>(o + n, lim);
             MChunk m;
             m.block = b;
-            m.start = (uint32_t)(o + s);
-            m.len = (uint32_t)std::min<uint64_t>(kMtfChunk, n - s);
+            m.start = (uint32_t)gpos;
+            m.len = (uint32_t)(e - gpos);
             m.rel = (uint32_t)s;
             hc.push_back(m);
+            s = e - o;
         }
         for (uint64_t s = 0; s < n; s += 65536)
             hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
