@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -70,6 +71,24 @@ struct Ctx {
     hipEvent_t ev();
     int tbegin(const char *name);  // -1 when timing is off
     void tend(int idx);
+};
+
+// Host wall-clock of a phase (device work included when the phase synchronises), recorded
+// under "wall:<name>" when timing is enabled.
+struct WallPhase {
+    Ctx *c;
+    const char *name;
+    std::chrono::steady_clock::time_point t0;
+    WallPhase(Ctx *c_, const char *n) : c(c_), name(n), t0(std::chrono::steady_clock::now()) {}
+    ~WallPhase() { stop(); }
+    void stop()
+    {
+        if (!name || !c->timing) return;
+        KStat &k = c->stats[std::string("wall:") + name];
+        k.launches++;
+        k.ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        name = nullptr;
+    }
 };
 
 // Kernel launch on the context stream, bracketed by timing events when enabled.

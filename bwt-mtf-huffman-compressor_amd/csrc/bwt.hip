@@ -33,14 +33,16 @@ namespace bmh {
 namespace {
 
 // ---------------------------------------------------------------------------- constants
-constexpr uint32_t kGBits = 12;                 // global pass digit width
-constexpr uint32_t kGBins = 1u << kGBits;       // 4096 buckets per block
-constexpr uint32_t kGChunk = 65536;             // positions per global-pass workgroup
-constexpr uint32_t kFinCap = 4096;              // max segment a finish workgroup sorts
+constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass workgroup (LDS-staged)
+constexpr uint32_t kBigCap = 17280;             // max segment of the big finish (9 B/elem + 8 KB LDS)
+constexpr uint32_t kBigNT = 1024, kBigIPT = (kBigCap + kBigNT - 1) / kBigNT;
+constexpr uint32_t kBigDigit = 12;              // LDS digit of the big finish
+constexpr uint32_t kFinCap = 4096;              // max segment a (small) finish workgroup sorts
 constexpr uint32_t kFinNT = 256, kFinIPT = kFinCap / kFinNT;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kFinKeyBits = 40;            // bits consumed by one finish pass (8 + 32)
-constexpr uint32_t kDataMaxBits = 64;           // deeper ties go to rank doubling
+constexpr uint32_t kDataMaxBits = 64;           // deeper MSD ties go to rank doubling
+constexpr uint32_t kFinMaxBits = 256;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
 // doubling phase
 constexpr uint32_t kTinyMax = 128;
@@ -102,11 +104,16 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
     const uint32_t B = db >> 3, sh = db & 7u;
     uint64_t w = 0;
     uint32_t x;
-    if ((uint64_t)p + B + 9 <= n) {
+    if ((uint64_t)p + B + 12 <= n) {
+        // three aligned dwords cover the 9 bytes [q, q + 9); none lies past q + 12
         const uint8_t *q = blk + p + B;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) w = (w << 8) | q[i];
-        x = q[8];
+        const uint32_t *aq = (const uint32_t *)((uintptr_t)q & ~(uintptr_t)3);
+        const uint32_t al = (uint32_t)((uintptr_t)q & 3u) * 8u;
+        const uint32_t d0 = aq[0], d1 = aq[1], d2 = aq[2];
+        const uint64_t lo = ((uint64_t)d1 << 32) | d0;
+        const uint64_t v = al ? ((lo >> al) | ((uint64_t)d2 << (64 - al))) : lo;
+        x = (d2 >> al) & 255u;
+        w = __builtin_bswap64(v);
     } else {
         uint64_t s = ((uint64_t)p + B) % n;
         for (int i = 0; i < 8; ++i) {
@@ -119,117 +126,274 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
     return w;
 }
 
-// ------------------------------------------------------------------- global 12-bit pass
-__device__ __forceinline__ uint32_t digit12(const uint8_t *__restrict__ blk, uint32_t n, uint32_t p)
+// A tied run of m > kSmallM rotations, grouped up to bit depth nd: another finish pass, or
+// rank doubling once it is deep (long repeats), or final when nd covers the whole rotation.
+__device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, uint32_t m, uint32_t nd, uint32_t b,
+                                              uint32_t n)
 {
-    const uint32_t q = p + 1 == n ? 0 : p + 1;
-    return ((uint32_t)blk[p] << 4) | (blk[q] >> 4);
+    if (nd >= 8ull * n) {
+        a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, m, nd, b | kFinalFlag);
+    } else if (nd >= kFinMaxBits) {
+        a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, m, nd, b);
+        a.bflag[b] = 1;
+    } else {
+        a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gs, m, nd, b);
+    }
 }
 
-// grid = chunk list (XCD-interleaved; pad entries have len 0); 1024 threads.
-__global__ __launch_bounds__(1024) void k_g12_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
-                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
+// ----------------------------------------------------------- global pass: first byte
+// Chunks of <= 16 K positions whose batch boundaries are 16-byte multiples (a block's first
+// chunk takes the unaligned prefix), dealt into 8 XCD lanes so one block's chunks share an L2.
+__device__ __forceinline__ void g1_load16(const uint8_t *__restrict__ blk, uint32_t start, uint32_t len, uint32_t e,
+                                          uint32_t (&dg)[4])
 {
-    __shared__ uint32_t h[kGBins];
+    // bytes [start + e, start + e + 16) of the block, zero past len
+    if (e + 16 <= len && (((uintptr_t)(blk + start + e)) & 15u) == 0) {
+        const uint4 v = *(const uint4 *)(blk + start + e);
+        dg[0] = v.x;
+        dg[1] = v.y;
+        dg[2] = v.z;
+        dg[3] = v.w;
+    } else {
+        dg[0] = dg[1] = dg[2] = dg[3] = 0;
+        for (uint32_t k = 0; k < 16; ++k)
+            if (e + k < len) dg[k >> 2] |= (uint32_t)blk[start + e + k] << (8 * (k & 3));
+    }
+}
+
+// grid = chunk list; 1024 threads x 16 positions.
+__global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
+                                                  const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
+{
+    __shared__ uint32_t h[16][256];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
-    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) h[i] = 0;
+    const uint32_t t = threadIdx.x, w = t >> 6;
+    for (uint32_t i = t; i < 16 * 256; i += 1024) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
-    const uint8_t *blk = data + boff;
-    for (uint32_t e = threadIdx.x; e < ch.len; e += 1024) atomicAdd(&h[digit12(blk, n, ch.start + e)], 1u);
+    const uint8_t *blk = data + boffs[ch.block];
+    const uint32_t e = 16 * t;
+    if (e < ch.len) {
+        uint32_t dg[4];
+        g1_load16(blk, ch.start, ch.len, e, dg);
+        const uint32_t nv = min(16u, ch.len - e);
+        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][(dg[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+    }
     __syncthreads();
-    uint32_t *out = chist + (size_t)blockIdx.x * kGBins;
-    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) out[i] = h[i];
-}
-
-// grid = nblocks; 1024 threads. Per digit: exclusive prefix over the block's chunks (in place,
-// -> block-relative write offsets), bucket table bk[b][d] = {start, len}; buckets larger than
-// a finish workgroup go to the MSD list.
-__global__ __launch_bounds__(1024) void k_g12_scan(const uint32_t *__restrict__ boffs, uint32_t nb,
-                                                   const uint32_t *__restrict__ bchunks, const uint32_t *__restrict__ bchunk0,
-                                                   uint32_t *__restrict__ chist, uint2 *__restrict__ bk, Seg4 *big,
-                                                   Counters *cnt)
-{
-    __shared__ uint32_t s_tmp[17];
-    const uint32_t b = blockIdx.x;
-    const uint32_t boff = boffs[b];
-    const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // chunk list indices c0 + 8k (XCD lane stride)
-    uint32_t carry = 0;
-    for (uint32_t r = 0; r < kGBins / 1024; ++r) {
-        const uint32_t d = r * 1024 + threadIdx.x;
+    if (t < 256) {
         uint32_t tot = 0;
-        for (uint32_t k = 0; k < nc; ++k) tot += chist[(size_t)(c0 + 8 * k) * kGBins + d];
-        uint32_t total;
-        const uint32_t start = carry + block_excl_sum<1024>(tot, s_tmp, &total);
-        uint32_t acc = start;
-        for (uint32_t k = 0; k < nc; ++k) {
-            uint32_t *h = &chist[(size_t)(c0 + 8 * k) * kGBins + d];
-            const uint32_t v = *h;
-            *h = acc;
-            acc += v;
-        }
-        bk[(size_t)b * kGBins + d] = make_uint2(start, tot);
-        if (tot > kFinCap) big[atomicAdd(&cnt->big, 1u)] = make_uint4(boff + start, tot, kGBits, b);
-        carry += total;
+        for (int k = 0; k < 16; ++k) tot += h[k][t];
+        chist[(size_t)blockIdx.x * 256 + t] = tot;
     }
 }
 
-__global__ __launch_bounds__(1024) void k_g12_scatter(DataArgs a, const GChunk *__restrict__ chunks,
-                                                      const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk)
+// grid = nblocks; 256 threads (digits): per-chunk write offsets (block-relative, in place),
+// bucket table bk8[b][d] = {start, len}; buckets too big for a finish workgroup -> MSD list.
+__global__ __launch_bounds__(256) void k_g1_scan(const uint32_t *__restrict__ boffs, const uint32_t *__restrict__ bchunks,
+                                                 const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
+                                                 uint2 *__restrict__ bk8, Seg4 *big, Counters *cnt)
 {
-    __shared__ uint32_t cur[kGBins];
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t b = blockIdx.x, d = threadIdx.x;
+    const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // list indices c0 + 8k (XCD lane stride)
+    uint32_t run = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+        uint32_t *h = &chist[(size_t)(c0 + 8 * k) * 256 + d];
+        const uint32_t v = *h;
+        *h = run;
+        run += v;
+    }
+    const uint32_t start = block_excl_sum<256>(run, s_tmp, nullptr);
+    for (uint32_t k = 0; k < nc; ++k) chist[(size_t)(c0 + 8 * k) * 256 + d] += start;
+    bk8[(size_t)b * 256 + d] = make_uint2(start, run);
+    if (run > kBigCap) big[atomicAdd(&cnt->big, 1u)] = make_uint4(boffs[b] + start, run, 8, b);
+}
+
+// Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs.
+__global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *__restrict__ chunks,
+                                                     const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk8)
+{
+    __shared__ uint32_t s_ent[kG1Chunk];  // (chunk-relative position << 8) | digit
+    __shared__ uint32_t s_cnt[256], s_ls[256], s_off[256], s_blen[256];
+    __shared__ uint32_t s_tmp[17];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
-    const uint32_t *in = chist + (size_t)blockIdx.x * kGBins;
-    for (uint32_t i = threadIdx.x; i < kGBins; i += 1024) cur[i] = in[i];
-    __syncthreads();
-    const uint32_t b = ch.block;
-    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t t = threadIdx.x;
+    const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    const uint2 *bkb = bk + (size_t)b * kGBins;
-    for (uint32_t e = threadIdx.x; e < ch.len; e += 1024) {
-        const uint32_t p = ch.start + e;
-        const uint32_t d = digit12(blk, n, p);
-        const uint32_t slot = atomicAdd(&cur[d], 1u);
+    if (t < 256) {
+        s_cnt[t] = 0;
+        s_off[t] = chist[(size_t)blockIdx.x * 256 + t];
+        s_blen[t] = bk8[(size_t)b * 256 + t].y;
+    }
+    __syncthreads();
+    const uint32_t e0 = 16 * t;
+    uint32_t dg[4] = {0, 0, 0, 0};
+    const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
+    if (nv) {
+        g1_load16(blk, ch.start, ch.len, e0, dg);
+        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&s_cnt[(dg[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+    }
+    __syncthreads();
+    {
+        // every wave takes part in the scan (it synchronises); digits live in threads 0..255
+        const uint32_t ex = block_excl_sum<1024>(t < 256 ? s_cnt[t] : 0u, s_tmp, nullptr);
+        if (t < 256) {
+            s_ls[t] = ex;
+            s_cnt[t] = ex;
+        }
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < nv; ++k) {
+        const uint32_t d = (dg[k >> 2] >> (8 * (k & 3))) & 255u;
+        const uint32_t dst = atomicAdd(&s_cnt[d], 1u);
+        s_ent[dst] = ((e0 + k) << 8) | d;
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < ch.len; i += 1024) {
+        const uint32_t v = s_ent[i], p = ch.start + (v >> 8), d = v & 255u;
+        const uint32_t slot = s_off[d] + (i - s_ls[d]);
         a.sa[boff + slot] = p;
-        if (bkb[d].y == 1) put_final(a, b, boff, n, blk, boff + slot, p, slot);  // singleton bucket
+        if (s_blen[d] == 1) put_final(a, b, boff, n, blk, boff + slot, p, slot);
     }
 }
 
-// ------------------------------------------------------------------------- finish pass
-// dense = 1: workgroup i -> (block, bucket) of the global pass, XCD-aware (i % 8 = lane of
-// blocks b = lane mod 8). dense = 0: one workgroup per list entry.
-__global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restrict__ list, const uint2 *__restrict__ bk,
-                                                int dense)
+// ------------------------------------------------------------------- big finish pass
+// One 1024-thread workgroup per segment of <= kBigCap positions at bit depth db (dense = 1:
+// the byte buckets of the global pass, XCD-aware: workgroup i -> lane i % 8 -> blocks
+// b = lane mod 8). All global gathers (SA entry, rotation window, last-column byte) are
+// issued together up front; LDS counting sort by the next 12 bits; then each sub-bucket of
+// <= 64 is ordered by the next 32 bits by rank counting (bit depth db + 44), larger ones are
+// deferred. 12-bit counters are packed two per word (16-bit halves; segment < 65536).
+__global__ __launch_bounds__(kBigNT) void k_finish_big(DataArgs a, const Seg4 *__restrict__ list,
+                                                       const uint2 *__restrict__ bk8, int dense)
 {
-    __shared__ uint32_t s_pos[kFinCap], s_rest[kFinCap];
-    __shared__ uint8_t s_dig[kFinCap];
-    __shared__ uint32_t s_cnt[256], s_start[257];
-    __shared__ uint32_t s_tmp[8];
+    __shared__ uint32_t s_pos[kBigCap], s_rest[kBigCap];
+    __shared__ uint8_t s_lb[kBigCap];
+    __shared__ uint32_t s_cnt[1u << (kBigDigit - 1)];
+    __shared__ uint32_t s_tmp[17];
     uint32_t gstart, len, db, b;
     if (dense) {
         const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
-        b = x + 8u * (k >> kGBits);
+        b = x + 8u * (k >> 8);
         if (b >= a.nb) return;
-        const uint2 e = bk[(size_t)b * kGBins + (k & (kGBins - 1))];
+        const uint2 e = bk8[(size_t)b * 256 + (k & 255u)];
         len = e.y;
-        if (len < 2 || len > kFinCap) return;
+        if (len < 2 || len > kBigCap) return;
         gstart = a.boffs[b] + e.x;
-        db = kGBits;
+        db = 8;
     } else {
         const Seg4 s = list[blockIdx.x];
         gstart = s.x;
         len = s.y;
         db = s.z;
         b = s.w;
+        if (len <= kFinCap) return;  // the small finish kernel takes it
     }
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < (1u << (kBigDigit - 1)); i += kBigNT) s_cnt[i] = 0;
+    __syncthreads();
+    uint32_t pv[kBigIPT], dv[kBigIPT], rv[kBigIPT], lv[kBigIPT];
+#pragma unroll
+    for (uint32_t k = 0; k < kBigIPT; ++k) {
+        const uint32_t e = t + k * kBigNT;
+        if (e < len) {
+            const uint32_t p = a.sa[gstart + e];
+            const uint64_t w = rot_window(blk, n, p, db);
+            pv[k] = p;
+            lv[k] = lastcol_byte(blk, n, p);
+            dv[k] = (uint32_t)(w >> (64 - kBigDigit));
+            rv[k] = (uint32_t)(w >> (32 - kBigDigit));
+            atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
+        }
+    }
+    __syncthreads();
+    {
+        // thread t owns digits 4t .. 4t + 3 (words 2t, 2t + 1)
+        const uint32_t w0 = s_cnt[2 * t], w1 = s_cnt[2 * t + 1];
+        const uint32_t c0 = w0 & 0xffffu, c1 = w0 >> 16, c2 = w1 & 0xffffu, c3 = w1 >> 16;
+        const uint32_t ex = block_excl_sum<kBigNT>(c0 + c1 + c2 + c3, s_tmp, nullptr);
+        s_cnt[2 * t] = ex | ((ex + c0) << 16);
+        s_cnt[2 * t + 1] = (ex + c0 + c1) | ((ex + c0 + c1 + c2) << 16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kBigIPT; ++k) {
+        const uint32_t e = t + k * kBigNT;
+        if (e < len) {
+            const uint32_t sh = 16 * (dv[k] & 1u);
+            const uint32_t dst = (atomicAdd(&s_cnt[dv[k] >> 1], 1u << sh) >> sh) & 0xffffu;
+            s_pos[dst] = pv[k];
+            s_rest[dst] = rv[k];
+            s_lb[dst] = (uint8_t)lv[k];
+        }
+    }
+    __syncthreads();
+    // s_cnt now holds the end of every sub-bucket
+    const uint64_t newbits = (uint64_t)db + kBigDigit + 32;
+    const bool final_depth = newbits >= 8ull * n;
+    for (uint32_t d = t; d < (1u << kBigDigit); d += kBigNT) {
+        const uint32_t s1 = (s_cnt[d >> 1] >> (16 * (d & 1u))) & 0xffffu;
+        const uint32_t s0 = d ? (s_cnt[(d - 1) >> 1] >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
+        const uint32_t m = s1 - s0;
+        if (m == 0) continue;
+        if (m == 1) {
+            const uint32_t p = s_pos[s0], slot = gstart + s0;
+            a.sa[slot] = p;
+            a.L[slot] = s_lb[s0];
+            if (p == 0) a.prim[b] = slot - boff;
+            continue;
+        }
+        if (m > kSmallM) {
+            for (uint32_t e = s0; e < s1; ++e) a.sa[gstart + e] = s_pos[e];
+            defer_segment(a, gstart + s0, m, db + kBigDigit, b, n);
+            continue;
+        }
+        for (uint32_t e = s0; e < s1; ++e) {
+            const uint32_t r = s_rest[e], p = s_pos[e];
+            uint32_t lt = 0, eqb = 0, eqt = 0;
+            for (uint32_t f = s0; f < s1; ++f) {
+                const uint32_t rf = s_rest[f];
+                lt += rf < r;
+                const bool eq = rf == r;
+                eqt += eq;
+                eqb += eq && f < e;
+            }
+            const uint32_t slot = gstart + s0 + lt + eqb;
+            const uint32_t gs = gstart + s0 + lt;
+            a.sa[slot] = p;
+            if (eqt == 1 || final_depth) {
+                a.L[slot] = s_lb[e];
+                if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+            }
+            if (eqt > 1 && eqb == 0) {
+                a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
+                    make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
+                if (!final_depth) a.bflag[b] = 1;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------- finish pass
+// One workgroup per list segment of <= 4096 positions (larger ones: k_finish_big).
+__global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restrict__ list)
+{
+    __shared__ uint32_t s_pos[kFinCap], s_rest[kFinCap];
+    __shared__ uint8_t s_dig[kFinCap], s_lb[kFinCap];
+    __shared__ uint32_t s_cnt[256], s_start[257];
+    __shared__ uint32_t s_tmp[8];
+    const Seg4 sg = list[blockIdx.x];
+    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
+    if (len > kFinCap) return;  // k_finish_big takes it
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     const uint32_t tid = threadIdx.x;
     s_cnt[tid] = 0;
     __syncthreads();
-    uint32_t pv[kFinIPT], rv[kFinIPT], dv[kFinIPT];
+    uint32_t pv[kFinIPT], rv[kFinIPT], dv[kFinIPT], lv[kFinIPT];
 #pragma unroll
     for (uint32_t k = 0; k < kFinIPT; ++k) {
         const uint32_t e = tid + k * kFinNT;
@@ -237,6 +401,7 @@ __global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restri
             const uint32_t p = a.sa[gstart + e];
             const uint64_t w = rot_window(blk, n, p, db);
             pv[k] = p;
+            lv[k] = lastcol_byte(blk, n, p);
             dv[k] = (uint32_t)(w >> 56);
             rv[k] = (uint32_t)(w >> 24);
             atomicAdd(&s_cnt[dv[k]], 1u);
@@ -260,6 +425,7 @@ __global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restri
             s_pos[dst] = pv[k];
             s_rest[dst] = rv[k];
             s_dig[dst] = (uint8_t)dv[k];
+            s_lb[dst] = (uint8_t)lv[k];
         }
     }
     __syncthreads();
@@ -271,15 +437,12 @@ __global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restri
         const uint32_t p = s_pos[e];
         if (m == 1) {
             a.sa[gstart + s0] = p;
-            put_final(a, b, boff, n, blk, gstart + s0, p, gstart + s0 - boff);
+            a.L[gstart + s0] = s_lb[e];
+            if (p == 0) a.prim[b] = gstart + s0 - boff;
         } else if (m > kSmallM) {
             a.sa[gstart + e] = p;  // deferred, still grouped by the 8-bit digit
             if (e == s0) {
-                const uint32_t nd = db + 8;
-                if (nd < 8ull * n)
-                    a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gstart + s0, m, nd, b);
-                else
-                    a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gstart + s0, m, nd, b | kFinalFlag);
+                defer_segment(a, gstart + s0, m, db + 8, b, n);
             }
         } else {
             const uint32_t r = s_rest[e];
@@ -292,17 +455,16 @@ __global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restri
                 eqb += eq && f < e;
             }
             const uint32_t slot = gstart + s0 + lt + eqb;
-            a.sa[slot] = p;
             const uint32_t gs = gstart + s0 + lt;
-            if (eqt == 1) {
-                put_final(a, b, boff, n, blk, slot, p, slot - boff);
-            } else {
-                if (final_depth) put_final(a, b, boff, n, blk, slot, p, gs - boff);
-                if (eqb == 0) {
-                    a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
-                        make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
-                    if (!final_depth) a.bflag[b] = 1;
-                }
+            a.sa[slot] = p;
+            if (eqt == 1 || final_depth) {
+                a.L[slot] = s_lb[e];
+                if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+            }
+            if (eqt > 1 && eqb == 0) {
+                a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
+                    make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
+                if (!final_depth) a.bflag[b] = 1;
             }
         }
     }
@@ -357,7 +519,7 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
         if (final_depth || nd >= kDataMaxBits) {
             a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u));
             if (!final_depth) a.bflag[b] = 1;
-        } else if (len <= kFinCap) {
+        } else if (len <= kBigCap) {
             a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gs, len, nd, b);
         } else {
             a.big_next[atomicAdd(&a.cnt->big_next, 1u)] = make_uint4(gs, len, nd, b);
@@ -898,14 +1060,22 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     const uint32_t nb = bt.nblocks;
     const uint64_t N = bt.total;
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
+    WallPhase wall_data(c, "bwt_data");
 
     // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8)
     std::vector<uint32_t> hoffs(nb + 1);
     for (uint32_t b = 0; b <= nb; ++b) hoffs[b] = (uint32_t)bt.offs[b];
     std::vector<std::vector<GChunk>> lane(8);
     for (uint32_t b = 0; b < nb; ++b) {
+        // the first chunk takes the unaligned prefix so the others start on 16-byte addresses
         const uint32_t n = hoffs[b + 1] - hoffs[b];
-        for (uint32_t s = 0; s < n; s += kGChunk) lane[b & 7].push_back(GChunk{b, s, std::min(kGChunk, n - s), 0});
+        const uint32_t mis = (uint32_t)(((uintptr_t)d_in + hoffs[b]) & 15u);
+        uint32_t s = 0, l = std::min(n, kG1Chunk - mis);
+        while (s < n) {
+            lane[b & 7].push_back(GChunk{b, s, l, 0});
+            s += l;
+            l = std::min(n - s, kG1Chunk);
+        }
     }
     size_t lmax = 0;
     for (auto &l : lane) lmax = std::max(lmax, l.size());
@@ -941,8 +1111,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
-    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kGBins * 4);
-    uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kGBins * 8);
+    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * 256 * 4);
+    uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * 256 * 8);
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list
     Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, seg_cap * 16);
@@ -975,12 +1145,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
 
     // ---- data phase
-    BMH_LAUNCH(c, "bwt_g12_hist", k_g12_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-    BMH_LAUNCH(c, "bwt_g12_scan", k_g12_scan, nb, 1024, 0, d_boffs, nb, d_bchunks, d_bchunk0, chist, bk, big, d_cnt);
-    BMH_LAUNCH(c, "bwt_g12_scatter", k_g12_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk);
+    BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
+    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, 256, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, big, d_cnt);
+    BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk);
     da.fin_next = fin_cur;
     da.big_next = big2;
-    BMH_LAUNCH(c, "bwt_finish", k_finish, 8u * cdiv(nb, 8) * kGBins, kFinNT, 0, da, nullptr, bk, 1);
+    BMH_LAUNCH(c, "bwt_finish_big", k_finish_big, 8u * cdiv(nb, 8) * 256, kBigNT, 0, da, nullptr, bk, 1);
     read_counters();
     uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
     Seg4 *big_cur = big, *big_nxt = big2;
@@ -993,7 +1163,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         if (nfin > 0) {
             da.fin_next = fin_nxt;
             da.big_next = big_nxt;
-            BMH_LAUNCH(c, "bwt_finish", k_finish, nfin, kFinNT, 0, da, fin_cur, bk, 0);
+            BMH_LAUNCH(c, "bwt_finish", k_finish, nfin, kFinNT, 0, da, fin_cur);
+            BMH_LAUNCH(c, "bwt_finish_big", k_finish_big, nfin, kBigNT, 0, da, fin_cur, bk, 0);
         }
         if (nbig > 0) {
             hs.resize(nbig);
@@ -1025,6 +1196,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     }
 
     // ---- doubling phase, only if some block still holds tied groups
+    wall_data.stop();
+    WallPhase wall_dbl(c, "bwt_doubling");
     const uint32_t ngroups = h_cnt->dgroups;
     if (ngroups > 0) {
         uint32_t *rkA = (uint32_t *)c->get(WS_RKA, N * 4);

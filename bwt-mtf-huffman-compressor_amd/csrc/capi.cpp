@@ -128,9 +128,16 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     uint8_t *d_L = (uint8_t *)c->get(WS_L, bt.total);
     uint8_t *d_mtf = (uint8_t *)c->get(WS_MTF, bt.total);
     std::vector<uint64_t> prim(nb);
-    bwt_batch(c, d_in, bt, d_L, prim.data());
+    {
+        WallPhase w(c, "bwt");
+        bwt_batch(c, d_in, bt, d_L, prim.data());
+    }
     std::vector<uint32_t> f32((size_t)nb * 256), fi32((size_t)nb * 256);
-    mtf_batch(c, d_L, bt, d_mtf, f32.data(), fi32.data());
+    {
+        WallPhase w(c, "mtf");
+        mtf_batch(c, d_L, bt, d_mtf, f32.data(), fi32.data());
+    }
+    WallPhase wt(c, "tables+pack");
 
     std::vector<bmh_code_table> tabs(nb);
     std::vector<uint64_t> pay(nb);
