@@ -45,7 +45,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_COUNT_
 };
 
 struct Ctx {
@@ -64,10 +64,21 @@ struct Ctx {
     // pinned host staging
     void *pinned = nullptr;
     size_t pinned_size = 0;
+    // pinned upload/download arena: every small host<->device copy goes through it so the
+    // copies stay asynchronous; reset at each sync()
+    uint8_t *arena = nullptr;
+    size_t arena_size = 0, arena_used = 0;
+    struct Deferred {
+        void *dst;
+        size_t off, bytes;
+    };
+    std::vector<Deferred> deferred;
 
     void *get(Slot s, size_t bytes);
     void *host_pinned(size_t bytes);
-    void sync();  // stream sync + resolve timing events
+    void h2d(void *d_dst, const void *h_src, size_t bytes);  // staged, asynchronous
+    void d2h(void *h_dst, const void *d_src, size_t bytes);  // staged; h_dst valid after sync()
+    void sync();  // stream sync (spin-wait) + staged downloads + timing events
     hipEvent_t ev();
     int tbegin(const char *name);  // -1 when timing is off
     void tend(int idx);

@@ -82,9 +82,52 @@ void Ctx::tend(int idx)
     BMH_HIP(hipEventRecord(pending[idx].b, stream));
 }
 
+static size_t arena_take(Ctx *c, size_t bytes)
+{
+    const size_t need = (bytes + 255) & ~(size_t)255;
+    if (c->arena_used + need > c->arena_size) {
+        c->sync();
+        if (need > c->arena_size) {
+            if (c->arena) BMH_HIP(hipHostFree(c->arena));
+            c->arena = nullptr;
+            const size_t sz = std::max<size_t>(need, 16u << 20);
+            BMH_HIP(hipHostMalloc((void **)&c->arena, sz, hipHostMallocDefault));
+            c->arena_size = sz;
+        }
+    }
+    const size_t off = c->arena_used;
+    c->arena_used += need;
+    return off;
+}
+
+void Ctx::h2d(void *d_dst, const void *h_src, size_t bytes)
+{
+    if (!bytes) return;
+    const size_t off = arena_take(this, bytes);
+    memcpy(arena + off, h_src, bytes);
+    BMH_HIP(hipMemcpyAsync(d_dst, arena + off, bytes, hipMemcpyHostToDevice, stream));
+}
+
+void Ctx::d2h(void *h_dst, const void *d_src, size_t bytes)
+{
+    if (!bytes) return;
+    const size_t off = arena_take(this, bytes);
+    BMH_HIP(hipMemcpyAsync(arena + off, d_src, bytes, hipMemcpyDeviceToHost, stream));
+    deferred.push_back(Deferred{h_dst, off, bytes});
+}
+
 void Ctx::sync()
 {
-    BMH_HIP(hipStreamSynchronize(stream));
+    // spin on the stream: a blocking wait can sleep the host thread for milliseconds, and
+    // the encode path synchronises a handful of times per batch
+    for (;;) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) BMH_HIP(e);
+    }
+    for (auto &d : deferred) memcpy(d.dst, arena + d.off, d.bytes);
+    deferred.clear();
+    arena_used = 0;
     for (auto &p : pending) {
         float ms = 0.f;
         BMH_HIP(hipEventElapsedTime(&ms, p.a, p.b));

@@ -279,9 +279,9 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     MChunk *d_chunks = (MChunk *)d_tab;
     HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
     uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));
-    BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(MChunk), hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_hh, hh.data(), nhh * sizeof(HChunk), hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_cfirst, cfirst.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    c->h2d(d_chunks, hc.data(), nch * sizeof(MChunk));
+    c->h2d(d_hh, hh.data(), nhh * sizeof(HChunk));
+    c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
     uint32_t *d_S = (uint32_t *)c->get(WS_MTF_S, (size_t)nch * 256);
@@ -294,8 +294,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_compose", k_mtf_compose, nb, 64, 0, d_cfirst, d_R, d_dcount, d_S);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_freq, d_first);
-    if (h_freq32) BMH_HIP(hipMemcpyAsync(h_freq32, d_freq, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    if (h_first32) BMH_HIP(hipMemcpyAsync(h_first32, d_first, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
+    if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     c->sync();
 }
 

@@ -162,9 +162,9 @@ void write_headers(Ctx *c, uint8_t *d_out, const std::vector<uint8_t> &hdr_bytes
     uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, hb + (nb + 1) * 16 + 64);
     uint64_t *d_src = (uint64_t *)(d_hdr + ((hb + 15) & ~(size_t)15));
     uint64_t *d_rec = d_src + (nb + 1);
-    BMH_HIP(hipMemcpyAsync(d_hdr, hdr_bytes.data(), hb, hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_src, src_offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_rec, rec_offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    c->h2d(d_hdr, hdr_bytes.data(), hb);
+    c->h2d(d_src, src_offs.data(), (nb + 1) * 8);
+    c->h2d(d_rec, rec_offs.data(), (nb + 1) * 8);
     BMH_LAUNCH(c, "pack_headers", k_headers, nb, 64, 0, d_hdr, d_src, d_rec, d_out);
     c->sync();  // host vectors may be released by the caller
 }
@@ -190,14 +190,14 @@ void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_f
     uint64_t *d_offs = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + 15) & ~(size_t)15));
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
-    BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(PChunk), hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_offs, bt.offs.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    c->h2d(d_chunks, hc.data(), nch * sizeof(PChunk));
+    c->h2d(d_offs, bt.offs.data(), (nb + 1) * 8);
     BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
     BMH_LAUNCH(c, "hist_fill", k_fill, (uint32_t)(((size_t)nb * 256 + 255) / 256), 256, 0, d_first, 0xffffffffu,
                (size_t)nb * 256);
     BMH_LAUNCH(c, "histogram", k_histogram, nch, 256, 0, d_in, d_chunks, d_offs, d_freq, d_first);
-    BMH_HIP(hipMemcpyAsync(h_freq32, d_freq, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
-    BMH_HIP(hipMemcpyAsync(h_first32, d_first, (size_t)nb * 256 * 4, hipMemcpyDeviceToHost, c->stream));
+    c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
+    c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     c->sync();
 }
 
@@ -235,10 +235,10 @@ void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_ta
     uint32_t *d_cfirst = (uint32_t *)(d_meta + nch * sizeof(PChunk));
     uint64_t *d_pay = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + (nb + 1) * 4 + 15) & ~(size_t)15));
     uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
-    BMH_HIP(hipMemcpyAsync(d_tab, ht.data(), nb * sizeof(DevTable), hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_chunks, hc.data(), nch * sizeof(PChunk), hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_cfirst, cfirst.data(), (nb + 1) * 4, hipMemcpyHostToDevice, c->stream));
-    BMH_HIP(hipMemcpyAsync(d_pay, pay_offs, nb * 8, hipMemcpyHostToDevice, c->stream));
+    c->h2d(d_tab, ht.data(), nb * sizeof(DevTable));
+    c->h2d(d_chunks, hc.data(), nch * sizeof(PChunk));
+    c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
+    c->h2d(d_pay, pay_offs, nb * 8);
     BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits);
     BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
     BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits, d_pay, (uint32_t *)d_out);
