@@ -39,8 +39,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # batch once per launch (DESIGN.md §4 states and justifies each figure).
 ALGO_BYTES_PER_INPUT_BYTE = {
     "bwt_g1_hist": 1.0,         # read input
-    "bwt_g1_scatter": 5.0,      # read input 1 B, write SA 4 B
-    "bwt_finish_big": 10.0,     # read SA 4 B, text 1 B, write SA 4 B, write L 1 B
+    "bwt_g1_scatter": 13.0,     # read input 1 B, write SA 4 B + rotation key 8 B
+    "bwt_finish_dense": 17.0,   # read SA 4 B + key 8 B, write SA 4 B + L 1 B
     "mtf_encode": 2.0,          # read L 1 B, write MTF 1 B
     "mtf_recency": 1.0,         # read L
     "mtf_hist": 1.0,            # read MTF

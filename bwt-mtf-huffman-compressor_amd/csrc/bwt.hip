@@ -34,13 +34,15 @@ namespace {
 
 // ---------------------------------------------------------------------------- constants
 constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass workgroup (LDS-staged)
-constexpr uint32_t kBigCap = 19072;             // max segment of the big finish (8.125 B/elem + 8 KB LDS)
-constexpr uint32_t kBigNT = 1024, kBigIPT = (kBigCap + kBigNT - 1) / kBigNT;
-constexpr uint32_t kBigDigit = 12;              // LDS digit of the big finish
-constexpr uint32_t kFinCap = 4096;              // max segment a (small) finish workgroup sorts
-constexpr uint32_t kFinNT = 256, kFinIPT = kFinCap / kFinNT;
+constexpr uint32_t kG1Bits = 10;                // global-pass digit: first byte + 2 bits
+constexpr uint32_t kG1Bins = 1u << kG1Bits;
+constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passes
+constexpr uint32_t kSegKeyBits = kSegDigit + 32;  // bits one finish pass resolves
+// finish workgroup shapes: dense (global-pass buckets), list small, list big
+constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
+constexpr uint32_t kFinNT = 256, kFinCap = 4096;
+constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
-constexpr uint32_t kFinKeyBits = 40;            // bits consumed by one finish pass (8 + 32)
 constexpr uint32_t kDataMaxBits = 64;           // deeper MSD ties go to rank doubling
 constexpr uint32_t kFinMaxBits = 256;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
@@ -141,9 +143,10 @@ __device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, ui
     }
 }
 
-// ----------------------------------------------------------- global pass: first byte
-// Chunks of <= 16 K positions whose batch boundaries are 16-byte multiples (a block's first
-// chunk takes the unaligned prefix), dealt into 8 XCD lanes so one block's chunks share an L2.
+// ------------------------------------------------------------------------- global pass
+// Counting sort of every block by its first kG1Bits rotation bits. Chunks of <= 16 K
+// positions whose batch boundaries are 16-byte multiples (a block's first chunk takes the
+// unaligned prefix), dealt into 8 XCD lanes so one block's chunks share an L2.
 __device__ __forceinline__ void g1_load16(const uint8_t *__restrict__ blk, uint32_t start, uint32_t len, uint32_t e,
                                           uint32_t (&dg)[4])
 {
@@ -161,76 +164,91 @@ __device__ __forceinline__ void g1_load16(const uint8_t *__restrict__ blk, uint3
     }
 }
 
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&dg)[4], uint32_t k)
+{
+    return (dg[k >> 2] >> (8 * (k & 3))) & 255u;
+}
+
+// digit of chunk element k (< nv) from its byte and the next one (nx = the byte after the run)
+__device__ __forceinline__ uint32_t g1_digit(const uint32_t (&dg)[4], uint32_t k, uint32_t nv, uint32_t nx)
+{
+    const uint32_t b1 = k + 1 < nv ? byte_of(dg, k + 1) : nx;
+    return (byte_of(dg, k) << (kG1Bits - 8)) | (b1 >> (16 - kG1Bits));
+}
+
 // grid = chunk list; 1024 threads x 16 positions.
 __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
 {
-    __shared__ uint32_t h[16][256];
+    __shared__ uint32_t h[4][kG1Bins];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
-    const uint32_t t = threadIdx.x, w = t >> 6;
-    for (uint32_t i = t; i < 16 * 256; i += 1024) (&h[0][0])[i] = 0;
+    const uint32_t t = threadIdx.x, w = (t >> 6) & 3u;
+    for (uint32_t i = t; i < 4 * kG1Bins; i += 1024) (&h[0][0])[i] = 0;
     __syncthreads();
-    const uint8_t *blk = data + boffs[ch.block];
+    const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
+    const uint8_t *blk = data + boff;
     const uint32_t e = 16 * t;
     if (e < ch.len) {
         uint32_t dg[4];
         g1_load16(blk, ch.start, ch.len, e, dg);
         const uint32_t nv = min(16u, ch.len - e);
-        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][(dg[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+        const uint32_t nx = blk[(uint32_t)(((uint64_t)ch.start + e + nv) % n)];
+        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx)], 1u);
     }
     __syncthreads();
-    if (t < 256) {
-        uint32_t tot = 0;
-        for (int k = 0; k < 16; ++k) tot += h[k][t];
-        chist[(size_t)blockIdx.x * 256 + t] = tot;
-    }
+    for (uint32_t d = t; d < kG1Bins; d += 1024)
+        chist[(size_t)blockIdx.x * kG1Bins + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
-// grid = nblocks; 256 threads (digits): per-chunk write offsets (block-relative, in place),
-// bucket table bk8[b][d] = {start, len}; buckets too big for a finish workgroup -> MSD list.
-__global__ __launch_bounds__(256) void k_g1_scan(const uint32_t *__restrict__ boffs, const uint32_t *__restrict__ bchunks,
-                                                 const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
-                                                 uint2 *__restrict__ bk8, Seg4 *big, Counters *cnt)
+// grid = nblocks; one thread per digit: per-chunk write offsets (block-relative, in place),
+// bucket table bk[b][d] = {start, len}; routing of buckets too big for a dense workgroup.
+__global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs,
+                                                     const uint32_t *__restrict__ bchunks,
+                                                     const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
+                                                     uint2 *__restrict__ bk, Seg4 *fin, Seg4 *big, Counters *cnt)
 {
-    __shared__ uint32_t s_tmp[8];
+    __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
     const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // list indices c0 + 8k (XCD lane stride)
     uint32_t run = 0;
     for (uint32_t k = 0; k < nc; ++k) {
-        uint32_t *h = &chist[(size_t)(c0 + 8 * k) * 256 + d];
+        uint32_t *h = &chist[(size_t)(c0 + 8 * k) * kG1Bins + d];
         const uint32_t v = *h;
         *h = run;
         run += v;
     }
-    const uint32_t start = block_excl_sum<256>(run, s_tmp, nullptr);
-    for (uint32_t k = 0; k < nc; ++k) chist[(size_t)(c0 + 8 * k) * 256 + d] += start;
-    bk8[(size_t)b * 256 + d] = make_uint2(start, run);
-    if (run > kBigCap) big[atomicAdd(&cnt->big, 1u)] = make_uint4(boffs[b] + start, run, 8, b);
+    const uint32_t start = block_excl_sum<kG1Bins>(run, s_tmp, nullptr);
+    for (uint32_t k = 0; k < nc; ++k) chist[(size_t)(c0 + 8 * k) * kG1Bins + d] += start;
+    bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
+    if (run > kBigCap)
+        big[atomicAdd(&cnt->big, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+    else if (run > kDenseCap)
+        fin[atomicAdd(&cnt->fin_next, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
 // together with each rotation's 8-byte key: bits 63..8 = rotation bytes 1..7 (big-endian),
 // bits 7..0 = the last-column byte. The chunk's text (with a cyclic halo) is staged in LDS,
-// so the keys cost no global gathers; the big finish pass reads them coalesced.
+// so the keys cost no global gathers; the dense finish pass reads them coalesced.
 __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *__restrict__ chunks,
-                                                     const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk8,
+                                                     const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk,
                                                      uint64_t *__restrict__ key8)
 {
     __shared__ uint16_t s_ent[kG1Chunk];  // chunk-relative position
     // byte j <-> block position start - 4 + j (cyclic), j < len + 12
     __shared__ uint32_t s_txt[(kG1Chunk + 12) / 4 + 1];
-    __shared__ uint32_t s_cnt[256], s_ls[256], s_off[256], s_blen[256];
+    __shared__ uint32_t s_cnt[kG1Bins], s_ls[kG1Bins], s_off[kG1Bins], s_blen[kG1Bins];
     __shared__ uint32_t s_tmp[17];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
     const uint32_t t = threadIdx.x;
     const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    if (t < 256) {
-        s_cnt[t] = 0;
-        s_off[t] = chist[(size_t)blockIdx.x * 256 + t];
-        s_blen[t] = bk8[(size_t)b * 256 + t].y;
+    for (uint32_t d = t; d < kG1Bins; d += 1024) {
+        s_cnt[d] = 0;
+        s_off[d] = chist[(size_t)blockIdx.x * kG1Bins + d];
+        s_blen[d] = bk[(size_t)b * kG1Bins + d].y;
     }
     {
         const uint32_t nw = (ch.len + 12 + 3) / 4;
@@ -253,40 +271,44 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     }
     __syncthreads();
     const uint32_t e0 = 16 * t;
-    uint32_t dg[4] = {0, 0, 0, 0};
+    uint32_t dg[4] = {0, 0, 0, 0}, nx = 0;
     const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
     if (nv) {
-        // bytes e0 .. e0 + 15 of the chunk = s_txt bytes e0 + 4 .. e0 + 19 (dword aligned)
+        // bytes e0 .. e0 + 16 of the chunk = s_txt bytes e0 + 4 .. e0 + 20 (dword aligned)
         for (int k = 0; k < 4; ++k) dg[k] = s_txt[(e0 >> 2) + 1 + k];
-        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&s_cnt[(dg[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+        if (nv < 16) {
+            const uint32_t j = e0 + 4 + nv;
+            nx = (s_txt[j >> 2] >> (8 * (j & 3u))) & 255u;
+            for (uint32_t k = nv; k < 16; ++k) dg[k >> 2] &= ~(255u << (8 * (k & 3)));
+        } else {
+            nx = s_txt[(e0 >> 2) + 5] & 255u;
+        }
+        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&s_cnt[g1_digit(dg, k, nv, nx)], 1u);
     }
     __syncthreads();
     {
-        // every wave takes part in the scan (it synchronises); digits live in threads 0..255
-        const uint32_t ex = block_excl_sum<1024>(t < 256 ? s_cnt[t] : 0u, s_tmp, nullptr);
-        if (t < 256) {
-            s_ls[t] = ex;
-            s_cnt[t] = ex;
-        }
+        static_assert(kG1Bins == 1024, "one digit per thread");
+        const uint32_t ex = block_excl_sum<1024>(s_cnt[t], s_tmp, nullptr);
+        s_ls[t] = ex;
+        s_cnt[t] = ex;
     }
     __syncthreads();
     for (uint32_t k = 0; k < nv; ++k) {
-        const uint32_t d = (dg[k >> 2] >> (8 * (k & 3))) & 255u;
-        const uint32_t dst = atomicAdd(&s_cnt[d], 1u);
+        const uint32_t dst = atomicAdd(&s_cnt[g1_digit(dg, k, nv, nx)], 1u);
         s_ent[dst] = (uint16_t)(e0 + k);
     }
     __syncthreads();
     for (uint32_t i = t; i < ch.len; i += 1024) {
         const uint32_t rel = s_ent[i];
         const uint32_t p = ch.start + rel;
-        // s_txt bytes rel + 3 .. rel + 11: L byte, byte p (the digit), bytes p + 1 .. p + 7
+        // s_txt bytes rel + 3 .. rel + 11: L byte, byte p, bytes p + 1 .. p + 7
         const uint32_t j0 = rel + 3, w0 = j0 >> 2, al = (j0 & 3u) * 8u;
         const uint32_t d0 = s_txt[w0], d1 = s_txt[w0 + 1], d2 = s_txt[w0 + 2];
         const uint64_t lo = ((uint64_t)d1 << 32) | d0;
         const uint64_t v64 = al ? ((lo >> al) | ((uint64_t)d2 << (64 - al))) : lo;  // bytes j0 .. j0 + 7
         const uint64_t b8 = (d2 >> al) & 255u;                                       // byte j0 + 8
         const uint64_t key = __builtin_bswap64((v64 >> 16) | (b8 << 48)) | (v64 & 255u);
-        const uint32_t d = (uint32_t)(v64 >> 8) & 255u;
+        const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
         const uint32_t slot = s_off[d] + (i - s_ls[d]);
         a.sa[boff + slot] = p;
         key8[boff + slot] = key;
@@ -297,14 +319,15 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     }
 }
 
-// ------------------------------------------------------------------- big finish pass
-// One 1024-thread workgroup per segment of <= kBigCap positions at bit depth db (dense = 1:
-// the byte buckets of the global pass, XCD-aware: workgroup i -> lane i % 8 -> blocks
-// b = lane mod 8). SA entries and rotation windows are gathered together up front; LDS
-// counting sort by the next 12 bits; then every element (one lane each, consecutive
+// ------------------------------------------------------------------------- finish pass
+// One workgroup of NT threads sorts one segment of <= CAP tied rotations (equal in bits
+// [0, db)). dense = 1: the buckets of the global pass (db = kG1Bits), XCD-aware: workgroup
+// i -> lane i % 8 -> blocks b = lane mod 8, keys read coalesced from key8. dense = 0: the
+// list entries with lo < len <= CAP, rotation windows gathered from the text.
+// LDS counting sort by the next 12 bits, then every element (one lane each, consecutive
 // elements in a wave) ranks itself inside its sub-bucket by the next 32 bits (bit depth
 // db + 44). Sub-bucket bounds come from a head bitmap; sub-buckets > kSmallM are deferred.
-// 12-bit counters are packed two per word (16-bit halves; segment < 65536).
+// 12-bit counters are packed two per word (16-bit halves; segments < 65536).
 __device__ __forceinline__ uint32_t bm_head_le(const uint32_t *bm, uint32_t i)
 {
     // highest set bit <= i (bit 0 is always set)
@@ -328,89 +351,88 @@ __device__ __forceinline__ uint32_t bm_head_gt(const uint32_t *bm, uint32_t i, u
     return min(len, w * 32 + (uint32_t)__builtin_ctz(bits));
 }
 
-__global__ __launch_bounds__(kBigNT) void k_finish_big(DataArgs a, const Seg4 *__restrict__ list,
-                                                       const uint2 *__restrict__ bk8, const uint64_t *__restrict__ key8,
-                                                       int dense, int dbg)
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
+                                                   const uint2 *__restrict__ bk, const uint64_t *__restrict__ key8,
+                                                   uint32_t lo, int dense)
 {
-    __shared__ uint32_t s_pos[kBigCap], s_rest[kBigCap];
-    __shared__ uint32_t s_cnt[1u << (kBigDigit - 1)];
-    __shared__ uint32_t s_bm[(kBigCap + 31) / 32 + 1];
-    __shared__ uint32_t s_tmp[17];
+    constexpr uint32_t IPT = (CAP + NT - 1) / NT;
+    constexpr uint32_t NDIG = 1u << kSegDigit, WPT = NDIG / 2 / NT;  // counter words per thread
+    static_assert(CAP < 65536 && WPT >= 1 && NDIG / 2 == WPT * NT, "finish shape");
+    __shared__ uint32_t s_pos[CAP], s_rest[CAP];
+    __shared__ uint32_t s_cnt[NDIG / 2];
+    __shared__ uint32_t s_bm[CAP / 32 + 2];
+    __shared__ uint32_t s_tmp[NT / 64 + 1];
     uint32_t gstart, len, db, b;
     if (dense) {
         const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
-        b = x + 8u * (k >> 8);
+        b = x + 8u * (k >> kG1Bits);
         if (b >= a.nb) return;
-        const uint2 e = bk8[(size_t)b * 256 + (k & 255u)];
+        const uint2 e = bk[(size_t)b * kG1Bins + (k & (kG1Bins - 1))];
         len = e.y;
-        if (len < 2 || len > kBigCap) return;
+        if (len < 2 || len > CAP) return;
         gstart = a.boffs[b] + e.x;
-        db = 8;
+        db = kG1Bits;
     } else {
         const Seg4 s = list[blockIdx.x];
         gstart = s.x;
         len = s.y;
         db = s.z;
         b = s.w;
-        if (len <= kFinCap) return;  // the small finish kernel takes it
+        if (len <= lo || len > CAP) return;
     }
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < (1u << (kBigDigit - 1)); i += kBigNT) s_cnt[i] = 0;
-    for (uint32_t i = t; i < (kBigCap + 31) / 32 + 1; i += kBigNT) s_bm[i] = 0;
+    for (uint32_t i = t; i < NDIG / 2; i += NT) s_cnt[i] = 0;
+    for (uint32_t i = t; i < CAP / 32 + 2; i += NT) s_bm[i] = 0;
     __syncthreads();
-    // dense: keys from the global pass, and the last-column byte rides in s_pos when
-    // positions fit 24 bits; list segments gather rotation windows (and L at the end)
+    // dense: the last-column byte rides in s_pos when positions fit 24 bits; otherwise (and
+    // for list segments) it is gathered at the end
     const bool packL = dense && n <= (1u << 24);
-    uint32_t pv[kBigIPT], dv[kBigIPT], rv[kBigIPT];
-    if (dense) {
+    uint32_t pv[IPT], dv[IPT], rv[IPT];
 #pragma unroll
-        for (uint32_t k = 0; k < kBigIPT; ++k) {
-            const uint32_t e = t + k * kBigNT;
-            if (e < len) {
-                const uint32_t p = a.sa[gstart + e];
-                const uint64_t w = key8[gstart + e];
-                pv[k] = packL ? (p << 8) | (uint32_t)(w & 255u) : p;
-                dv[k] = (uint32_t)(w >> (64 - kBigDigit));
-                rv[k] = (uint32_t)(w >> (32 - kBigDigit));
-                atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
-            }
-        }
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < kBigIPT; ++k) {
-            const uint32_t e = t + k * kBigNT;
-            if (e < len) {
-                const uint32_t p = a.sa[gstart + e];
-                const uint64_t w = rot_window(blk, n, p, db);
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t e = t + k * NT;
+        if (e < len) {
+            const uint32_t p = a.sa[gstart + e];
+            uint64_t w;
+            if (dense) {
+                const uint64_t key = key8[gstart + e];
+                w = key << (kG1Bits - 8);
+                pv[k] = packL ? (p << 8) | (uint32_t)(key & 255u) : p;
+            } else {
+                w = rot_window(blk, n, p, db);
                 pv[k] = p;
-                dv[k] = (uint32_t)(w >> (64 - kBigDigit));
-                rv[k] = (uint32_t)(w >> (32 - kBigDigit));
-                atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
             }
+            dv[k] = (uint32_t)(w >> (64 - kSegDigit));
+            rv[k] = (uint32_t)(w >> (32 - kSegDigit));
+            atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
         }
     }
     __syncthreads();
-    if (dbg == 1) return;
     {
-        // thread t owns digits 4t .. 4t + 3 (words 2t, 2t + 1); marks the sub-bucket heads
-        const uint32_t w0 = s_cnt[2 * t], w1 = s_cnt[2 * t + 1];
-        const uint32_t c[4] = {w0 & 0xffffu, w0 >> 16, w1 & 0xffffu, w1 >> 16};
-        uint32_t ex = block_excl_sum<kBigNT>(c[0] + c[1] + c[2] + c[3], s_tmp, nullptr);
-        uint32_t st[4];
-        for (int j = 0; j < 4; ++j) {
-            st[j] = ex;
-            if (c[j]) atomicOr(&s_bm[ex >> 5], 1u << (ex & 31u));
-            ex += c[j];
+        // thread t owns counter words WPT*t .. WPT*t + WPT - 1; marks the sub-bucket heads
+        uint32_t c[2 * WPT], sum = 0;
+        for (uint32_t j = 0; j < WPT; ++j) {
+            const uint32_t w = s_cnt[WPT * t + j];
+            c[2 * j] = w & 0xffffu;
+            c[2 * j + 1] = w >> 16;
+            sum += c[2 * j] + c[2 * j + 1];
         }
-        s_cnt[2 * t] = st[0] | (st[1] << 16);
-        s_cnt[2 * t + 1] = st[2] | (st[3] << 16);
+        uint32_t ex = block_excl_sum<NT>(sum, s_tmp, nullptr);
+        for (uint32_t j = 0; j < WPT; ++j) {
+            const uint32_t e0 = ex, e1 = ex + c[2 * j];
+            if (c[2 * j]) atomicOr(&s_bm[e0 >> 5], 1u << (e0 & 31u));
+            if (c[2 * j + 1]) atomicOr(&s_bm[e1 >> 5], 1u << (e1 & 31u));
+            s_cnt[WPT * t + j] = e0 | (e1 << 16);
+            ex = e1 + c[2 * j + 1];
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < kBigIPT; ++k) {
-        const uint32_t e = t + k * kBigNT;
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t e = t + k * NT;
         if (e < len) {
             const uint32_t sh = 16 * (dv[k] & 1u);
             const uint32_t dst = (atomicAdd(&s_cnt[dv[k] >> 1], 1u << sh) >> sh) & 0xffffu;
@@ -419,14 +441,13 @@ __global__ __launch_bounds__(kBigNT) void k_finish_big(DataArgs a, const Seg4 *_
         }
     }
     __syncthreads();
-    if (dbg == 2) return;
-    const uint64_t newbits = (uint64_t)db + kBigDigit + 32;
+    const uint64_t newbits = (uint64_t)db + kSegKeyBits;
     const bool final_depth = newbits >= 8ull * n;
-    // rank every element inside its sub-bucket; stores and last-column gathers afterwards
-    uint32_t sl[kBigIPT], lb[kBigIPT];
+    // rank every element inside its sub-bucket; last-column gathers and stores afterwards
+    uint32_t sl[IPT], lb[IPT];
 #pragma unroll
-    for (uint32_t k = 0; k < kBigIPT; ++k) {
-        const uint32_t e = t + k * kBigNT;
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t e = t + k * NT;
         sl[k] = 0xffffffffu;
         if (e < len) {
             const uint32_t s0 = bm_head_le(s_bm, e), s1 = bm_head_gt(s_bm, e, len), m = s1 - s0;
@@ -434,7 +455,7 @@ __global__ __launch_bounds__(kBigNT) void k_finish_big(DataArgs a, const Seg4 *_
             pv[k] = pe;
             if (m > kSmallM) {
                 a.sa[gstart + e] = p;  // deferred, grouped by the 12-bit digit
-                if (e == s0) defer_segment(a, gstart + s0, m, db + kBigDigit, b, n);
+                if (e == s0) defer_segment(a, gstart + s0, m, db + kSegDigit, b, n);
                 continue;
             }
             const uint32_t r = s_rest[e];
@@ -460,106 +481,12 @@ __global__ __launch_bounds__(kBigNT) void k_finish_big(DataArgs a, const Seg4 *_
             }
         }
     }
-    if (dbg == 3) return;
 #pragma unroll
-    for (uint32_t k = 0; k < kBigIPT; ++k)
+    for (uint32_t k = 0; k < IPT; ++k)
         if (sl[k] != 0xffffffffu) lb[k] = packL ? pv[k] & 255u : lastcol_byte(blk, n, pv[k]);
 #pragma unroll
-    for (uint32_t k = 0; k < kBigIPT; ++k)
+    for (uint32_t k = 0; k < IPT; ++k)
         if (sl[k] != 0xffffffffu) a.L[sl[k]] = (uint8_t)lb[k];
-}
-
-// ------------------------------------------------------------------------- finish pass
-// One workgroup per list segment of <= 4096 positions (larger ones: k_finish_big).
-__global__ __launch_bounds__(256) void k_finish(DataArgs a, const Seg4 *__restrict__ list)
-{
-    __shared__ uint32_t s_pos[kFinCap], s_rest[kFinCap];
-    __shared__ uint8_t s_dig[kFinCap], s_lb[kFinCap];
-    __shared__ uint32_t s_cnt[256], s_start[257];
-    __shared__ uint32_t s_tmp[8];
-    const Seg4 sg = list[blockIdx.x];
-    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
-    if (len > kFinCap) return;  // k_finish_big takes it
-    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-    const uint8_t *blk = a.data + boff;
-    const uint32_t tid = threadIdx.x;
-    s_cnt[tid] = 0;
-    __syncthreads();
-    uint32_t pv[kFinIPT], rv[kFinIPT], dv[kFinIPT], lv[kFinIPT];
-#pragma unroll
-    for (uint32_t k = 0; k < kFinIPT; ++k) {
-        const uint32_t e = tid + k * kFinNT;
-        if (e < len) {
-            const uint32_t p = a.sa[gstart + e];
-            const uint64_t w = rot_window(blk, n, p, db);
-            pv[k] = p;
-            lv[k] = lastcol_byte(blk, n, p);
-            dv[k] = (uint32_t)(w >> 56);
-            rv[k] = (uint32_t)(w >> 24);
-            atomicAdd(&s_cnt[dv[k]], 1u);
-        }
-    }
-    __syncthreads();
-    {
-        const uint32_t c = s_cnt[tid];
-        const uint32_t ex = block_excl_sum<kFinNT>(c, s_tmp, nullptr);
-        s_start[tid] = ex;
-        if (tid == kFinNT - 1) s_start[256] = ex + c;
-        __syncthreads();
-        s_cnt[tid] = ex;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < kFinIPT; ++k) {
-        const uint32_t e = tid + k * kFinNT;
-        if (e < len) {
-            const uint32_t dst = atomicAdd(&s_cnt[dv[k]], 1u);
-            s_pos[dst] = pv[k];
-            s_rest[dst] = rv[k];
-            s_dig[dst] = (uint8_t)dv[k];
-            s_lb[dst] = (uint8_t)lv[k];
-        }
-    }
-    __syncthreads();
-    const uint64_t newbits = (uint64_t)db + kFinKeyBits;
-    const bool final_depth = newbits >= 8ull * n;
-    for (uint32_t e = tid; e < len; e += kFinNT) {
-        const uint32_t d = s_dig[e];
-        const uint32_t s0 = s_start[d], m = s_start[d + 1] - s0;
-        const uint32_t p = s_pos[e];
-        if (m == 1) {
-            a.sa[gstart + s0] = p;
-            a.L[gstart + s0] = s_lb[e];
-            if (p == 0) a.prim[b] = gstart + s0 - boff;
-        } else if (m > kSmallM) {
-            a.sa[gstart + e] = p;  // deferred, still grouped by the 8-bit digit
-            if (e == s0) {
-                defer_segment(a, gstart + s0, m, db + 8, b, n);
-            }
-        } else {
-            const uint32_t r = s_rest[e];
-            uint32_t lt = 0, eqb = 0, eqt = 0;
-            for (uint32_t f = s0; f < s0 + m; ++f) {
-                const uint32_t rf = s_rest[f];
-                lt += rf < r;
-                const bool eq = rf == r;
-                eqt += eq;
-                eqb += eq && f < e;
-            }
-            const uint32_t slot = gstart + s0 + lt + eqb;
-            const uint32_t gs = gstart + s0 + lt;
-            a.sa[slot] = p;
-            if (eqt == 1 || final_depth) {
-                a.L[slot] = s_lb[e];
-                if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
-            }
-            if (eqt > 1 && eqb == 0) {
-                a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
-                    make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
-                if (!final_depth) a.bflag[b] = 1;
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -1153,7 +1080,6 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     const uint64_t N = bt.total;
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
     WallPhase wall_data(c, "bwt_data");
-    static const int dbg_mode = getenv("BMH_DBG_FINISH") ? atoi(getenv("BMH_DBG_FINISH")) : 0;
 
     // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8)
     std::vector<uint32_t> hoffs(nb + 1);
@@ -1205,8 +1131,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
     uint64_t *key8 = (uint64_t *)c->get(WS_KEY8, N * 8);
-    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * 256 * 4);
-    uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * 256 * 8);
+    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
+    uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list
     Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, seg_cap * 16);
@@ -1240,11 +1166,14 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     // ---- data phase
     BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, 256, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, big, d_cnt);
+    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, fin_cur, big,
+               d_cnt);
     BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, key8);
+    // the dense finish appends deferred segments after the global pass's list entries
     da.fin_next = fin_cur;
     da.big_next = big2;
-    BMH_LAUNCH(c, "bwt_finish_big", k_finish_big, 8u * cdiv(nb, 8) * 256, kBigNT, 0, da, nullptr, bk, key8, 1, dbg_mode);
+    BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_seg<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
+               da, nullptr, bk, key8, 0u, 1);
     read_counters();
     uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
     Seg4 *big_cur = big, *big_nxt = big2;
@@ -1257,8 +1186,10 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         if (nfin > 0) {
             da.fin_next = fin_nxt;
             da.big_next = big_nxt;
-            BMH_LAUNCH(c, "bwt_finish", k_finish, nfin, kFinNT, 0, da, fin_cur);
-            BMH_LAUNCH(c, "bwt_finish_big", k_finish_big, nfin, kBigNT, 0, da, fin_cur, bk, nullptr, 0, 0);
+            BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, bk, nullptr,
+                       1u, 0);
+            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfin, kBigNT, 0, da, fin_cur, bk,
+                       nullptr, kFinCap, 0);
         }
         if (nbig > 0) {
             hs.resize(nbig);
@@ -1404,7 +1335,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     c->d2h(h_prim, d_prim, nb * 4);
     c->sync();
     for (uint32_t b = 0; b < nb; ++b) {
-        if (h_prim[b] == 0xffffffffu && !dbg_mode) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
+        if (h_prim[b] == 0xffffffffu) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
         h_primary[b] = h_prim[b];
     }
 }
