@@ -45,7 +45,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_COUNT_
 };
 
 struct Ctx {
@@ -125,15 +125,27 @@ struct Batch {
 };
 Batch make_batch(const uint64_t *offs, uint32_t nblocks);
 
-// Stage implementations (device buffers, host-synchronous).
+// Per-block code book on the device (huffman.hip, pack.hip).
+struct DevTable {
+    uint64_t code[256];
+    uint8_t len[256];
+};
+// device status word bits (encode pipeline; checked by the host after the final sync)
+constexpr uint32_t kStatusEmpty = 1, kStatusCodeLen = 2, kStatusPrimary = 4, kStatusCapacity = 8;
+
+// Stage implementations (device buffers). bwt_batch / mtf_batch synchronise only when they
+// return host outputs (h_primary / h_freq32 non-null).
 void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,
                uint32_t *h_first32);
 void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
                 const uint64_t *pay_offs);
+void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint32_t *d_freq, const uint32_t *d_first,
+                    const uint32_t *d_prim, DevTable *d_tabs, uint64_t *d_roffs, uint64_t *d_pay_offs,
+                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status);
+void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
+                    uint8_t *d_out, const uint32_t *d_status);
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);
-void write_headers(Ctx *c, uint8_t *d_out, const std::vector<uint8_t> &hdr_bytes,
-                   const std::vector<uint64_t> &hdr_src_offs, const std::vector<uint64_t> &rec_offs);
 void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
 
 // Host Huffman (huffman_host.cpp)

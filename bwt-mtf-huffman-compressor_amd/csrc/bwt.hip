@@ -1331,6 +1331,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     }
 
     // ---- primary indices
+    if (!h_primary) return;  // the primaries stay on the device (WS_PRIMARY), checked there
     uint32_t *h_prim = (uint32_t *)c->host_pinned(nb * 4 + 4096);
     c->d2h(h_prim, d_prim, nb * 4);
     c->sync();

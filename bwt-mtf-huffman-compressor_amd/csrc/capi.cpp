@@ -167,74 +167,41 @@ uint64_t record_bound(uint64_t n) { return kRecordHeader + 320 + n + 16; }
 void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
                    uint64_t *rec_offs)
 {
+    // BWT -> MTF (+ histograms) -> code books, record offsets and headers -> bit pack, all
+    // on the context stream; the host waits on the BWT's list counters, and once at the end
     const uint32_t nb = bt.nblocks;
     uint8_t *d_L = (uint8_t *)c->get(WS_L, bt.total);
     uint8_t *d_mtf = (uint8_t *)c->get(WS_MTF, bt.total);
-    std::vector<uint64_t> prim(nb);
     {
         WallPhase w(c, "bwt");
-        bwt_batch(c, d_in, bt, d_L, prim.data());
+        bwt_batch(c, d_in, bt, d_L, nullptr);
     }
-    std::vector<uint32_t> f32((size_t)nb * 256), fi32((size_t)nb * 256);
     {
         WallPhase w(c, "mtf");
-        mtf_batch(c, d_L, bt, d_mtf, f32.data(), fi32.data());
+        mtf_batch(c, d_L, bt, d_mtf, nullptr, nullptr);
     }
-    WallPhase wt(c, "tables+pack");
-
-    std::vector<bmh_code_table> tabs(nb);
-    std::vector<uint64_t> pay(nb);
-    auto build = [&](uint32_t b0, uint32_t b1) {
-        for (uint32_t b = b0; b < b1; ++b) {
-            uint64_t freq[256], first[256];
-            for (int s = 0; s < 256; ++s) {
-                freq[s] = f32[(size_t)b * 256 + s];
-                const uint32_t f = fi32[(size_t)b * 256 + s];
-                first[s] = f == 0xffffffffu ? UINT64_MAX : f;
-            }
-            huffman_build(freq, first, &tabs[b]);
-            pay[b] = payload_bytes(&tabs[b], freq);
-        }
-    };
-    if (nb >= 64) {  // trees are independent: spread over a few host threads
-        const uint32_t nt = std::min<uint32_t>(8, std::max(1u, std::thread::hardware_concurrency()));
-        std::vector<std::thread> th;
-        std::vector<std::string> err(nt);
-        for (uint32_t t = 0; t < nt; ++t)
-            th.emplace_back([&, t]() {
-                try {
-                    build(nb * t / nt, nb * (t + 1) / nt);
-                } catch (const std::exception &e) {
-                    err[t] = e.what();
-                }
-            });
-        for (auto &x : th) x.join();
-        for (auto &e : err)
-            if (!e.empty()) fail(BMH_ERANGE, e);
-    } else {
-        build(0, nb);
-    }
-    rec_offs[0] = 0;
-    std::vector<uint64_t> src(nb + 1, 0), roffs(nb + 1, 0), pay_offs(nb);
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t hl = kRecordHeader + tabs[b].tree_len;
-        src[b + 1] = src[b] + hl;
-        roffs[b + 1] = roffs[b] + hl + pay[b];
-        pay_offs[b] = roffs[b] + hl;
-    }
-    if (roffs[nb] > out_cap) fail(BMH_ERANGE, "encode: output capacity too small");
-    std::vector<uint8_t> hdr(src[nb]);
-    for (uint32_t b = 0; b < nb; ++b) {
-        uint8_t *h = &hdr[src[b]];
-        put_u64(h, prim[b]);
-        put_u64(h + 8, bt.offs[b + 1] - bt.offs[b]);
-        put_u64(h + 16, tabs[b].tree_len);
-        memcpy(h + 24, tabs[b].tree, tabs[b].tree_len);
-    }
-    BMH_HIP(hipMemsetAsync(d_out, 0, roffs[nb], c->stream));
-    write_headers(c, d_out, hdr, src, roffs);
-    pack_batch(c, d_mtf, bt, tabs.data(), d_out, pay_offs.data());
-    for (uint32_t b = 0; b <= nb; ++b) rec_offs[b] = roffs[b];
+    WallPhase wt(c, "huffman+pack");
+    const uint32_t *d_prim = (const uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);
+    const uint32_t *d_freq = (const uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
+    const uint32_t *d_first = (const uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
+    DevTable *d_tabs = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
+    uint64_t *d_roffs = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 1) * 8 + 64);
+    uint64_t *d_pay_offs = d_roffs + nb + 1;
+    uint8_t *d_misc = (uint8_t *)c->get(WS_STATUS, (size_t)(nb + 1) * 8 + 64);
+    uint32_t *d_status = (uint32_t *)d_misc;
+    uint64_t *d_boffs = (uint64_t *)(d_misc + 64);
+    BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
+    c->h2d(d_boffs, bt.offs.data(), (nb + 1) * 8);
+    codebook_batch(c, bt, d_boffs, d_freq, d_first, d_prim, d_tabs, d_roffs, d_pay_offs, d_out, out_cap, d_status);
+    pack_batch_dev(c, d_mtf, bt, d_tabs, d_pay_offs, d_out, d_status);
+    uint32_t st = 0;
+    c->d2h(rec_offs, d_roffs, (nb + 1) * 8);
+    c->d2h(&st, d_status, 4);
+    c->sync();
+    if (st & kStatusCapacity) fail(BMH_ERANGE, "encode: output capacity too small");
+    if (st & kStatusEmpty) fail(BMH_EINVAL, "huffman: empty histogram (the reference segfaults on empty input)");
+    if (st & kStatusCodeLen) fail(BMH_ERANGE, "huffman: code longer than 64 bits");
+    if (st & kStatusPrimary) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
 }
 
 static uint64_t max_batch_bytes()

@@ -1,0 +1,271 @@
+// huffman.hip — per-block Huffman code books and record layout on the device.
+//
+// Replaces the tree half of huffman() (reference main.cpp:229-257), traverse/build_hashmap
+// (main.cpp:132-156), dfs/tree_to_bytes (main.cpp:174-196) and the record header of
+// write_to_file (io_utilities.h:7-27) for a whole batch, so the encode pipeline never
+// round-trips histograms through the host. One wave per block:
+//   leaves   : symbols with freq > 0 ranked by first occurrence in the MTF stream
+//   tree     : the reference's std::priority_queue simulated exactly. Node ids: leaves
+//              0..L-1, internal nodes L, L+1, ... in creation order; a pop takes the
+//              smallest (freq, -addr_rank(id)) — equal frequencies leave the heap in
+//              descending glibc heap-address order (same model as
+//              huffman_host.cpp). Each pop is a wave-wide argmin over 512 register slots.
+//   codes    : DFS from the root (left = 0), preorder tree bits (internal 1, leaf 0 + 8
+//              value bits MSB-first), by lane 0.
+//   header   : [u64 primary][u64 n][u64 tree_len][tree bytes] staged per block.
+// k_rec_offs then scans header + payload sizes into record offsets (capacity checked on the
+// device), and k_rec_headers copies each header to its record.
+#include "bmh_internal.h"
+#include "device_util.h"
+
+namespace bmh {
+
+namespace {
+
+constexpr uint32_t kHdrStride = 352;  // 24 header bytes + <= 320 tree bytes, 16-aligned
+
+__device__ __forceinline__ uint32_t addr_rank(uint32_t L, uint32_t s)
+{
+    if (L <= 128) {
+        // [1, 3..127, 0, 2, 128, 129, ...]
+        if (s == 1) return 0;
+        if (s >= 3 && s <= 127) return s - 2;
+        if (s == 0) return 126;
+        if (s == 2) return 127;
+        return s;
+    }
+    // [1, 3..64, 129..192, 65..127, 0, 2, 128, 193, 194, ...]
+    if (s == 1) return 0;
+    if (s >= 3 && s <= 64) return s - 2;
+    if (s >= 129 && s <= 192) return s - 66;
+    if (s >= 65 && s <= 127) return s + 62;
+    if (s == 0) return 190;
+    if (s == 2) return 191;
+    if (s == 128) return 192;
+    return s;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
+{
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t heap_key(uint64_t freq, uint32_t L, uint32_t id)
+{
+    return (freq << 32) | (0xffffu - addr_rank(L, id));
+}
+
+// Removes the minimum key of the wave's 512 slots; returns its node id and frequency.
+__device__ __forceinline__ uint32_t heap_pop(uint64_t (&key)[8], uint64_t &freq)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t lm = key[0];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) lm = key[k] < lm ? key[k] : lm;
+    const uint64_t wm = wave_min_u64(lm);
+    uint32_t myid = 0;
+    bool found = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (key[k] == wm) {
+            key[k] = ~0ull;
+            myid = lane + 64u * k;
+            found = true;
+        }
+    const uint64_t bal = __ballot(found);
+    const int owner = __ffsll((long long)bal) - 1;
+    freq = wm >> 32;
+    return (uint32_t)__shfl((int)myid, owner, 64);
+}
+
+// grid = nblocks, 64 threads (one wave per block).
+__global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ freq32,
+                                                   const uint32_t *__restrict__ first32,
+                                                   const uint32_t *__restrict__ prim, const uint64_t *__restrict__ boffs,
+                                                   DevTable *__restrict__ tabs, uint8_t *__restrict__ hdr,
+                                                   uint32_t *__restrict__ hdr_len, uint64_t *__restrict__ pay_bytes,
+                                                   uint32_t *status)
+{
+    __shared__ uint32_t s_freq[256], s_first[256];
+    __shared__ uint8_t s_order[256];
+    __shared__ int16_t s_left[512], s_right[512];
+    __shared__ uint64_t s_code[256];
+    __shared__ uint8_t s_len[256];
+    __shared__ uint8_t s_tree[320];
+    __shared__ uint16_t s_stk_node[260];
+    __shared__ uint8_t s_stk_depth[260];
+    __shared__ uint64_t s_stk_code[260];
+    __shared__ uint32_t s_tree_bits, s_err;
+    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    for (uint32_t s = lane; s < 256; s += 64) {
+        s_freq[s] = freq32[(size_t)b * 256 + s];
+        s_first[s] = first32[(size_t)b * 256 + s];
+        s_len[s] = 0;
+        s_code[s] = 0;
+    }
+    for (uint32_t i = lane; i < 320; i += 64) s_tree[i] = 0;
+    if (lane == 0) s_err = 0;
+    __syncthreads();
+    // leaves in first-occurrence order (main.cpp:238-244); first positions are distinct
+    uint32_t L = 0;
+    for (uint32_t s = lane; s < 256; s += 64) L += s_freq[s] > 0;
+    for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+    for (uint32_t s = lane; s < 256; s += 64) {
+        if (!s_freq[s]) continue;
+        const uint32_t fs = s_first[s];
+        uint32_t r = 0;
+        for (uint32_t t = 0; t < 256; ++t) r += s_freq[t] > 0 && s_first[t] < fs;
+        s_order[r] = (uint8_t)s;
+    }
+    __syncthreads();
+    if (L == 0) {
+        if (lane == 0) atomicOr(status, kStatusEmpty);
+        return;
+    }
+    // the priority queue (main.cpp:245-254): first pop -> left child, second -> right
+    uint64_t key[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t id = lane + 64u * k;
+        key[k] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
+    }
+    for (uint32_t m = 0; m + 1 < L; ++m) {
+        uint64_t fa, fb;
+        const uint32_t a = heap_pop(key, fa);
+        const uint32_t c = heap_pop(key, fb);
+        const uint32_t v = L + m;
+        const uint64_t nk = heap_key(fa + fb, L, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (lane + 64u * k == v) key[k] = nk;
+        if (lane == 0) {
+            s_left[v] = (int16_t)a;
+            s_right[v] = (int16_t)c;
+        }
+    }
+    __syncthreads();
+    // codes (left 0, right 1; a root leaf gets the empty code) and preorder tree bits
+    if (lane == 0) {
+        const uint32_t root = L == 1 ? 0u : 2 * L - 2;
+        uint32_t sp = 0, bit = 0;
+        s_stk_node[0] = (uint16_t)root;
+        s_stk_depth[0] = 0;
+        s_stk_code[0] = 0;
+        sp = 1;
+        while (sp) {
+            --sp;
+            const uint32_t v = s_stk_node[sp], d = s_stk_depth[sp];
+            const uint64_t code = s_stk_code[sp];
+            if (v < L) {
+                const uint32_t sym = s_order[v];
+                if (d > 64) s_err |= kStatusCodeLen;
+                s_len[sym] = (uint8_t)d;
+                s_code[sym] = code;
+                // 0 then the 8 value bits
+                const uint32_t val = sym;
+                bit += 1;
+                for (int k = 7; k >= 0; --k, ++bit)
+                    if ((val >> k) & 1u) s_tree[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7u));
+            } else {
+                s_tree[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7u));
+                ++bit;
+                s_stk_node[sp] = (uint16_t)s_right[v];
+                s_stk_depth[sp] = (uint8_t)(d + 1);
+                s_stk_code[sp] = (code << 1) | 1u;
+                ++sp;
+                s_stk_node[sp] = (uint16_t)s_left[v];
+                s_stk_depth[sp] = (uint8_t)(d + 1);
+                s_stk_code[sp] = code << 1;
+                ++sp;
+            }
+        }
+        s_tree_bits = bit;
+    }
+    __syncthreads();
+    DevTable *t = &tabs[b];
+    uint64_t bits = 0;
+    for (uint32_t s = lane; s < 256; s += 64) {
+        t->code[s] = s_code[s];
+        t->len[s] = s_len[s];
+        bits += (uint64_t)s_freq[s] * s_len[s];
+    }
+    for (int off = 32; off >= 1; off >>= 1) bits += __shfl_xor(bits, off, 64);
+    const uint32_t tree_len = (s_tree_bits + 7) >> 3;
+    const uint64_t n = boffs[b + 1] - boffs[b];
+    const uint32_t p = prim[b];
+    uint8_t *h = hdr + (size_t)b * kHdrStride;
+    for (uint32_t i = lane; i < 24 + tree_len; i += 64) {
+        uint8_t v;
+        if (i < 8) v = (uint8_t)((uint64_t)p >> (8 * i));
+        else if (i < 16) v = (uint8_t)(n >> (8 * (i - 8)));
+        else if (i < 24) v = (uint8_t)((uint64_t)tree_len >> (8 * (i - 16)));
+        else v = s_tree[i - 24];
+        h[i] = v;
+    }
+    if (lane == 0) {
+        hdr_len[b] = 24 + tree_len;
+        const uint64_t pb = (bits + 7) / 8;
+        pay_bytes[b] = pb ? pb : 1;  // encode_with_huffman starts from one zero byte (main.cpp:162)
+        uint32_t e = s_err;
+        if (p == 0xffffffffu) e |= kStatusPrimary;
+        if (e) atomicOr(status, e);
+    }
+}
+
+// One workgroup: record offsets = exclusive scan of (header + payload) sizes.
+__global__ __launch_bounds__(1024) void k_rec_offs(uint32_t nb, const uint32_t *__restrict__ hdr_len,
+                                                   const uint64_t *__restrict__ pay_bytes, uint64_t *__restrict__ roffs,
+                                                   uint64_t *__restrict__ pay_offs, uint64_t out_cap, uint32_t *status)
+{
+    __shared__ uint64_t s_tmp[17];
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += 1024) {
+        const uint32_t b = base + threadIdx.x;
+        const uint64_t v = b < nb ? hdr_len[b] + pay_bytes[b] : 0ull;
+        uint64_t total;
+        const uint64_t ex = carry + block_excl_sum64<1024>(v, s_tmp, &total);
+        if (b < nb) {
+            roffs[b] = ex;
+            pay_offs[b] = ex + hdr_len[b];
+        }
+        carry += total;
+    }
+    if (threadIdx.x == 0) {
+        roffs[nb] = carry;
+        if (carry > out_cap) atomicOr(status, kStatusCapacity);
+    }
+}
+
+__global__ __launch_bounds__(64) void k_rec_headers(const uint8_t *__restrict__ hdr, const uint32_t *__restrict__ hdr_len,
+                                                    const uint64_t *__restrict__ roffs, uint8_t *__restrict__ out,
+                                                    const uint32_t *status)
+{
+    if (*status & kStatusCapacity) return;
+    const uint32_t b = blockIdx.x;
+    const uint8_t *h = hdr + (size_t)b * kHdrStride;
+    uint8_t *o = out + roffs[b];
+    for (uint32_t i = threadIdx.x; i < hdr_len[b]; i += 64) o[i] = h[i];
+}
+
+}  // namespace
+
+void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint32_t *d_freq, const uint32_t *d_first,
+                    const uint32_t *d_prim, DevTable *d_tabs, uint64_t *d_roffs, uint64_t *d_pay_offs,
+                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status)
+{
+    const uint32_t nb = bt.nblocks;
+    uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, (size_t)nb * kHdrStride + (size_t)nb * 12 + 64);
+    uint64_t *d_payb = (uint64_t *)(d_hdr + (size_t)nb * kHdrStride);
+    uint32_t *d_hlen = (uint32_t *)(d_payb + nb);
+    BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
+               d_status);
+    BMH_LAUNCH(c, "rec_offs", k_rec_offs, 1, 1024, 0, nb, d_hlen, d_payb, d_roffs, d_pay_offs, out_cap, d_status);
+    BMH_LAUNCH(c, "rec_headers", k_rec_headers, nb, 64, 0, d_hdr, d_hlen, d_roffs, d_out, d_status);
+}
+
+}  // namespace bmh

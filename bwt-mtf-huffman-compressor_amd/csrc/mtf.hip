@@ -296,7 +296,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_freq, d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
-    c->sync();
+    if (h_freq32 || h_first32) c->sync();
 }
 
 }  // namespace bmh

@@ -7,9 +7,11 @@
 //   scan   : per block, exclusive scan of chunk bit counts (u64)
 //   write  : per chunk, thread bit offsets by a workgroup scan; code words OR'd into an LDS
 //            image of the chunk's 32-bit big-endian words; interior words stored, the two
-//            edge words (shared with neighbouring chunks / record headers) atomicOr'd.
-// The output region is zeroed first; record headers + tree bytes (host-built) are copied in
-// by k_headers before the pack, and the payload of block b starts at byte pay_offs[b].
+//            edge words (shared with neighbouring chunks / record headers) updated under a
+//            mask of this chunk's bits (atomicAnd + atomicOr), so the output needs no
+//            zeroing pass. The block's last chunk owns the zero pad bits of its last byte.
+// Record headers are written before the pack (huffman.hip); the payload of block b starts
+// at byte pay_offs[b].
 #include "bmh_internal.h"
 #include "device_util.h"
 
@@ -21,11 +23,6 @@ namespace {
 
 constexpr uint32_t kPackChunk = 4096;  // symbols per workgroup (256 threads x 16)
 constexpr uint32_t kPackIPT = kPackChunk / 256;
-
-struct DevTable {
-    uint64_t code[256];
-    uint8_t len[256];
-};
 
 struct PChunk {
     uint32_t block, start, len, pad;
@@ -65,18 +62,22 @@ __global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ 
 __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ mtf, const PChunk *__restrict__ chunks,
                                                     const DevTable *__restrict__ tabs,
                                                     const uint64_t *__restrict__ cboff,
-                                                    const uint64_t *__restrict__ pay_offs, uint32_t *__restrict__ out)
+                                                    const uint64_t *__restrict__ pay_offs,
+                                                    const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ out,
+                                                    const uint32_t *status)
 {
     __shared__ uint64_t s_code[256];
     __shared__ uint8_t s_len[256];
     __shared__ uint64_t s_tmp[8];
     __shared__ uint32_t s_img[kPackChunk * 64 / 32 + 2];
+    if (status && (*status & kStatusCapacity)) return;
     const PChunk ch = chunks[blockIdx.x];
     const DevTable *t = &tabs[ch.block];
     s_code[threadIdx.x] = t->code[threadIdx.x];
     s_len[threadIdx.x] = t->len[threadIdx.x];
     __syncthreads();
-    const uint64_t G = pay_offs[ch.block] * 8 + cboff[blockIdx.x];  // global bit position
+    const uint64_t P = pay_offs[ch.block] * 8;   // the block's first payload bit
+    const uint64_t G = P + cboff[blockIdx.x];    // this chunk's first bit
     const uint64_t W0 = G >> 5;
     const uint32_t sh0 = (uint32_t)(G & 31u);
     uint8_t sym[kPackIPT];
@@ -89,8 +90,17 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     }
     uint64_t total;
     uint64_t tb = block_excl_sum64<256>(mybits, s_tmp, &total) + sh0;
-    if (total == 0) return;
-    const uint32_t nwords = (uint32_t)((sh0 + total + 31) >> 5);
+    // the block's last chunk also owns the zero pad bits up to the payload's last byte
+    // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
+    const bool last = blockIdx.x + 1 == cfirst[ch.block + 1];
+    uint64_t own_end = G + total;
+    if (last) {
+        const uint64_t bbits = cboff[blockIdx.x] + total;
+        const uint64_t pb = (bbits + 7) / 8;
+        own_end = P + 8 * (pb ? pb : 1);
+    }
+    if (own_end == G) return;
+    const uint32_t nwords = (uint32_t)((own_end - W0 * 32 + 31) >> 5);
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) s_img[w] = 0;
     __syncthreads();
     for (uint32_t k = 0; k < kPackIPT; ++k) {
@@ -107,10 +117,20 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
         }
     }
     __syncthreads();
+    // words wholly inside [G, own_end) are stored; the edge words are shared with the
+    // neighbouring chunks / record headers: only this chunk's bits are replaced, atomically
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) {
+        const uint64_t ws = (W0 + w) * 32;
+        const uint32_t a = G > ws ? (uint32_t)(G - ws) : 0u;
+        const uint32_t e = own_end < ws + 32 ? (uint32_t)(own_end - ws) : 32u;
         const uint32_t v = __builtin_bswap32(s_img[w]);
-        if (w == 0 || w == nwords - 1) atomicOr(&out[W0 + w], v);
-        else out[W0 + w] = v;
+        if (a == 0 && e == 32) {
+            out[W0 + w] = v;
+        } else {
+            const uint32_t m = __builtin_bswap32((0xffffffffu >> a) & (0xffffffffu << (32 - e)));
+            atomicAnd(&out[W0 + w], ~m);
+            atomicOr(&out[W0 + w], v & m);
+        }
     }
 }
 
@@ -143,31 +163,7 @@ __global__ void k_fill(uint32_t *p, uint32_t v, size_t n)
     if (i < n) p[i] = v;
 }
 
-// Copy host-built [u64 primary][u64 n][u64 tree_len][tree] prefixes to the record offsets.
-__global__ __launch_bounds__(64) void k_headers(const uint8_t *__restrict__ src, const uint64_t *__restrict__ src_offs,
-                                                const uint64_t *__restrict__ rec_offs, uint8_t *__restrict__ out)
-{
-    const uint32_t b = blockIdx.x;
-    const uint64_t s0 = src_offs[b], len = src_offs[b + 1] - s0;
-    for (uint32_t i = threadIdx.x; i < len; i += 64) out[rec_offs[b] + i] = src[s0 + i];
-}
-
 }  // namespace
-
-void write_headers(Ctx *c, uint8_t *d_out, const std::vector<uint8_t> &hdr_bytes, const std::vector<uint64_t> &src_offs,
-                   const std::vector<uint64_t> &rec_offs)
-{
-    const uint32_t nb = (uint32_t)rec_offs.size() - 1;
-    const size_t hb = hdr_bytes.size();
-    uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, hb + (nb + 1) * 16 + 64);
-    uint64_t *d_src = (uint64_t *)(d_hdr + ((hb + 15) & ~(size_t)15));
-    uint64_t *d_rec = d_src + (nb + 1);
-    c->h2d(d_hdr, hdr_bytes.data(), hb);
-    c->h2d(d_src, src_offs.data(), (nb + 1) * 8);
-    c->h2d(d_rec, rec_offs.data(), (nb + 1) * 8);
-    BMH_LAUNCH(c, "pack_headers", k_headers, nb, 64, 0, d_hdr, d_src, d_rec, d_out);
-    c->sync();  // host vectors may be released by the caller
-}
 
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32)
 {
@@ -201,18 +197,11 @@ void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_f
     c->sync();
 }
 
-void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
-                const uint64_t *pay_offs)
+void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
+                    uint8_t *d_out, const uint32_t *d_status)
 {
     if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const uint32_t nb = bt.nblocks;
-    std::vector<DevTable> ht(nb);
-    for (uint32_t b = 0; b < nb; ++b) {
-        memcpy(ht[b].code, tables[b].code, sizeof ht[b].code);
-        memcpy(ht[b].len, tables[b].len, sizeof ht[b].len);
-        for (int s = 0; s < 256; ++s)
-            if (tables[b].len[s] > 64) fail(BMH_ERANGE, "pack: code longer than 64 bits");
-    }
     std::vector<PChunk> hc;
     std::vector<uint32_t> cfirst(nb + 1);
     for (uint32_t b = 0; b < nb; ++b) {
@@ -229,19 +218,34 @@ void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_ta
     }
     cfirst[nb] = (uint32_t)hc.size();
     const uint32_t nch = (uint32_t)hc.size();
-    DevTable *d_tab = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
-    uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 4 + nb * 8 + 64);
+    uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 4 + 64);
     PChunk *d_chunks = (PChunk *)d_meta;
     uint32_t *d_cfirst = (uint32_t *)(d_meta + nch * sizeof(PChunk));
-    uint64_t *d_pay = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + (nb + 1) * 4 + 15) & ~(size_t)15));
     uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
-    c->h2d(d_tab, ht.data(), nb * sizeof(DevTable));
     c->h2d(d_chunks, hc.data(), nch * sizeof(PChunk));
     c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
-    c->h2d(d_pay, pay_offs, nb * 8);
-    BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits);
+    BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits);
     BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
-    BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tab, d_cbits, d_pay, (uint32_t *)d_out);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits, d_pay_offs, d_cfirst,
+               (uint32_t *)d_out, d_status);
+}
+
+void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
+                const uint64_t *pay_offs)
+{
+    const uint32_t nb = bt.nblocks;
+    std::vector<DevTable> ht(nb);
+    for (uint32_t b = 0; b < nb; ++b) {
+        memcpy(ht[b].code, tables[b].code, sizeof ht[b].code);
+        memcpy(ht[b].len, tables[b].len, sizeof ht[b].len);
+        for (int s = 0; s < 256; ++s)
+            if (tables[b].len[s] > 64) fail(BMH_ERANGE, "pack: code longer than 64 bits");
+    }
+    DevTable *d_tab = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
+    uint64_t *d_pay = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 1) * 8 + 64);
+    c->h2d(d_tab, ht.data(), nb * sizeof(DevTable));
+    c->h2d(d_pay, pay_offs, nb * 8);
+    pack_batch_dev(c, d_mtf, bt, d_tab, d_pay, d_out, nullptr);
     c->sync();
 }
 
