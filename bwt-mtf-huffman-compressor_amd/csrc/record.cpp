@@ -148,8 +148,16 @@ void bwt_inverse(const uint8_t *L, uint64_t n, uint64_t primary, uint8_t *out)
 
 uint64_t record_n(const uint8_t *rec, uint64_t len)
 {
+    // header sanity before anyone sizes a buffer from n
     if (len < kRecordHeader) fail(BMH_ECORRUPT, "record: shorter than its 24-byte header");
-    return get_u64(rec + 8);
+    const uint64_t n = get_u64(rec + 8), tlen = get_u64(rec + 16);
+    if (n == 0) fail(BMH_ECORRUPT, "record: n == 0");
+    if (tlen == 0 || tlen > len - kRecordHeader) fail(BMH_ECORRUPT, "record: tree length exceeds record");
+    if (get_u64(rec) >= n) fail(BMH_ECORRUPT, "record: primary index out of range");
+    // a root with two children gives every symbol a code of >= 1 bit
+    const uint64_t pay = len - kRecordHeader - tlen;
+    if ((rec[kRecordHeader] & 0x80u) && n / 8 > pay) fail(BMH_ECORRUPT, "record: n exceeds what the payload holds");
+    return n;
 }
 
 void record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out)

@@ -1,0 +1,142 @@
+"""CPU: the product library's host side, without a GPU.
+
+- libbmh.so loads and exports every function include/bmh.h declares;
+- host-only stages (Huffman code book, record decode, container framing, MTF decode) agree
+  with the reference's golden records;
+- every device entry point fails loudly (BMH_ENODEV) when no gfx950 device is present —
+  there is no CPU fallback in the product path.
+"""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import bmh
+from oracle_ffi import GOLDEN, golden_calgary, golden_small
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "bmh.h")
+CLI = os.path.join(REPO, "bwt-mtf-huffman-compressor_amd", "bin", "bmh")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = set(re.findall(r"\b(bmh_[a-z0-9_]+)\s*\(", txt))
+    return sorted(n for n in names if not n.endswith("_t"))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = bmh.lib()
+    names = _declared()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (bmh_\w+)", out))
+    assert set(names) <= exported
+
+
+def test_version_and_status_strings():
+    assert bmh.lib().bmh_version().decode().startswith("bmh ")
+    for st in range(7):
+        assert bmh.lib().bmh_status_str(st)
+
+
+def _hist(mtf: bytes):
+    a = np.frombuffer(mtf, np.uint8)
+    freq = np.bincount(a, minlength=256).astype(np.uint64)
+    first = np.full(256, np.iinfo(np.uint64).max, np.uint64)
+    idx = np.unique(a, return_index=True)
+    first[idx[0]] = idx[1]
+    return freq, first
+
+
+def test_huffman_build_reproduces_golden_trees():
+    """Host code book vs the reference's own tree bytes and payload sizes (App. B tie-break)."""
+    for name, data, rec in list(golden_calgary()) + list(golden_small()):
+        mtf = bmh.record_to_mtf(rec)
+        freq, first = _hist(mtf)
+        t = bmh.huffman_build(freq, first)
+        tl = int.from_bytes(rec[16:24], "little")
+        assert t.tree_len == tl, name
+        assert t.tree_bytes == rec[24:24 + tl], name
+        assert bmh.payload_bytes(t, freq) == len(rec) - 24 - tl, name
+
+
+def test_decompress_golden_records():
+    for name, data, rec in list(golden_calgary()) + list(golden_small()):
+        assert bmh.decompress_bytes(rec) == data, name
+
+
+def test_record_to_mtf_matches_oracle(oracle):
+    for name, data, rec in golden_calgary():
+        if len(data) > 200000:
+            continue
+        assert bmh.record_to_mtf(rec) == oracle.mtf(oracle.bwt(data)[1]), name
+
+
+def test_container_framing():
+    recs = [r for _, _, r in golden_small()]
+    datas = [d for _, d, _ in golden_small()]
+    bs = 1 << 20
+    body = b"".join(recs)
+    hdr = b"\xffBMHBLK1" + bs.to_bytes(8, "little") + len(recs).to_bytes(8, "little") + \
+        sum(map(len, datas)).to_bytes(8, "little") + b"".join(len(r).to_bytes(8, "little") for r in recs)
+    cont = hdr + body
+    assert bmh.is_container(cont) and not bmh.is_container(recs[0])
+    assert bmh.container_records(cont) == recs
+    assert bmh.decompress_bytes(cont) == b"".join(datas)
+
+
+@pytest.mark.parametrize("mutate", ["truncate", "bad_n", "bad_tree_len", "bad_primary"])
+def test_corrupt_records_fail_loudly(mutate):
+    _, data, rec = next(golden_calgary())
+    r = bytearray(rec)
+    if mutate == "truncate":
+        r = r[:100]
+    elif mutate == "bad_n":
+        r[8:16] = (10 ** 12).to_bytes(8, "little")
+    elif mutate == "bad_tree_len":
+        r[16:24] = (10 ** 6).to_bytes(8, "little")
+    else:
+        r[0:8] = (len(data) + 5).to_bytes(8, "little")
+    with pytest.raises(bmh.BmhError):
+        bmh.decompress_bytes(bytes(r))
+
+
+def test_metrics_line_matches_reference_stdout():
+    gold = {e["file"]: e["stdout_tail"] for e in json.load(open(os.path.join(GOLDEN, "calgary_stdout.json")))}
+    for name, data, rec in golden_calgary():
+        hdr = 24 + int.from_bytes(rec[16:24], "little")
+        line = bmh.metrics_line(name + ".bzap", len(data), len(rec), hdr) + "\n"
+        assert line.endswith(gold[name]), name
+
+
+@pytest.mark.skipif(bmh.lib().bmh_device_count() > 0, reason="a GPU is present")
+def test_device_paths_fail_loudly_without_gpu():
+    with pytest.raises(bmh.BmhError) as e:
+        bmh.Context(0)
+    assert e.value.status == 6  # BMH_ENODEV
+    with pytest.raises(bmh.BmhError):
+        bmh.bwt(b"banana")
+
+
+@pytest.mark.skipif(not os.path.exists(CLI), reason="CLI not built")
+def test_cli_host_modes(tmp_path):
+    # the per-mode aliases behave like the reference's per-mode binaries (main.cpp:439-451)
+    r = subprocess.run([CLI + "_compress", "only_one_arg"], capture_output=True, text=True)
+    assert r.returncode == 1 and r.stdout == "Wrong arguments. Pass only input and output file as parameters"
+    name, data, rec = next(golden_calgary())
+    src = tmp_path / "bib.bzap"
+    src.write_bytes(rec)
+    out = tmp_path / "bib.out"
+    r = subprocess.run([CLI, "decompress", str(src), str(out)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert out.read_bytes() == data
+    if bmh.lib().bmh_device_count() == 0:
+        r = subprocess.run([CLI, "compress", str(out), str(tmp_path / "x.bzap")], capture_output=True, text=True)
+        assert r.returncode != 0 and "device" in (r.stderr + r.stdout).lower()
