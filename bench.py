@@ -37,16 +37,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 # Algorithmic HBM bytes per input byte of the batch for the kernels that sweep the whole
 # batch once per launch (DESIGN.md §4 states and justifies each figure).
-ALGO_BYTES_PER_INPUT_BYTE = {
+# roofline.achieved uses SURVEY.md §8(d)'s graded per-unit figure: 1 algorithmic HBM byte per
+# input byte ("HBM-read roofline"), times the input bytes one launch processes. Every kernel
+# below processes the whole batch per launch. STAGE_BYTES_PER_INPUT_BYTE is the
+# diagnostic per-stage traffic model (minimum bytes each kernel must move).
+ALGO_BYTES_PER_INPUT_BYTE = 1.0
+STAGE_BYTES_PER_INPUT_BYTE = {
     "bwt_g1_hist": 1.0,         # read input
     "bwt_g1_scatter": 13.0,     # read input 1 B, write SA 4 B + rotation key 8 B
     "bwt_finish_dense": 17.0,   # read SA 4 B + key 8 B, write SA 4 B + L 1 B
-    "mtf_encode": 2.0,          # read L 1 B, write MTF 1 B
     "mtf_recency": 1.0,         # read L
+    "mtf_encode": 2.0,          # read L 1 B, write MTF 1 B
     "mtf_hist": 1.0,            # read MTF
     "pack_bits": 1.0,           # read MTF
     "pack_write": 2.0,          # read MTF 1 B, write payload ~1 B (random data)
 }
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def log(*a):
@@ -188,21 +194,27 @@ def main() -> None:
         value = in_bytes * steps / dt / 1e6
         # dominant kernel over the timed region
         dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
-        steps_k = ksteps
         roof = None
         if dom:
             name, (launches, ms) = dom
+            lps = launches / ksteps
             avg_s = ms / launches / 1e3
-            bpb = ALGO_BYTES_PER_INPUT_BYTE.get(name)
-            per_launch = bpb * total if bpb is not None else None
-            if per_launch is not None and name.startswith("bwt_tiny"):
-                per_launch = per_launch / max(1, launches / steps_k)  # several rounds per step
-            ach = per_launch / avg_s / 1e9 if per_launch else None
-            roof = {"bound": "hbm", "kernel": name, "achieved": round(ach, 2) if ach else None,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
-                    "traffic": None, "avg_launch_ms": round(avg_s * 1e3, 4),
-                    "launches_per_step": launches / steps_k,
-                    "algorithmic_bytes_per_launch": per_launch}
+            per_launch = ALGO_BYTES_PER_INPUT_BYTE * total / lps  # batch bytes per launch
+            ach = per_launch / avg_s / 1e9
+            traffic = None
+            try:  # HBM bytes per launch from the committed PMC summary of this workload
+                pm = json.load(open(PMC_TRAFFIC))
+                if pm.get("workload_bytes") == total and name in pm.get("kernels", {}):
+                    traffic = pm["kernels"][name]["hbm_bytes_per_launch"]
+            except (OSError, ValueError, KeyError):
+                pass
+            stage = STAGE_BYTES_PER_INPUT_BYTE.get(name)
+            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": lps,
+                    "algorithmic_bytes_per_launch": per_launch,
+                    "stage_model_bytes_per_launch": stage * total if stage else None,
+                    "stage_model_frac": round(stage * total / avg_s / 1e9 / HBM_PEAK_GBS, 4) if stage else None}
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
             "warmup": a.warmup, "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
