@@ -45,7 +45,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_COUNT_
 };
 
 struct Ctx {
@@ -130,6 +130,18 @@ struct DevTable {
     uint64_t code[256];
     uint8_t len[256];
 };
+inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Pack chunks: 4 K symbols, aligned to each block's start; mtf_batch writes one u16
+// histogram per pack chunk (WS_PACK_HIST), pack_batch_dev sizes the chunks from them.
+constexpr uint32_t kPackChunkSyms = 4096;
+inline void pack_chunk_first(const Batch &bt, uint32_t *first)
+{
+    first[0] = 0;
+    for (uint32_t b = 0; b < bt.nblocks; ++b)
+        first[b + 1] = first[b] + (uint32_t)((bt.offs[b + 1] - bt.offs[b] + kPackChunkSyms - 1) / kPackChunkSyms);
+}
+
 // device status word bits (encode pipeline; checked by the host after the final sync)
 constexpr uint32_t kStatusEmpty = 1, kStatusCodeLen = 2, kStatusPrimary = 4, kStatusCapacity = 8;
 
@@ -144,7 +156,7 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
                     const uint32_t *d_prim, DevTable *d_tabs, uint64_t *d_roffs, uint64_t *d_pay_offs,
                     uint8_t *d_out, uint64_t out_cap, uint32_t *d_status);
 void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
-                    uint8_t *d_out, const uint32_t *d_status);
+                    uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist);
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);
 void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
 

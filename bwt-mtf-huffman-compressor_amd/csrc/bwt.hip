@@ -1049,7 +1049,6 @@ __global__ void k_fill_u32(uint32_t *p, uint32_t v, uint32_t n)
     if (i < n) p[i] = v;
 }
 
-inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
 // Host-side tiling of a segment list into <= kDTile pieces.
 template <class S, class T>

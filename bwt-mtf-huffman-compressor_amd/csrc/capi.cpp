@@ -193,7 +193,8 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
     c->h2d(d_boffs, bt.offs.data(), (nb + 1) * 8);
     codebook_batch(c, bt, d_boffs, d_freq, d_first, d_prim, d_tabs, d_roffs, d_pay_offs, d_out, out_cap, d_status);
-    pack_batch_dev(c, d_mtf, bt, d_tabs, d_pay_offs, d_out, d_status);
+    const uint16_t *d_chist = (const uint16_t *)c->get(WS_PACK_HIST, 64);  // written by mtf_batch
+    pack_batch_dev(c, d_mtf, bt, d_tabs, d_pay_offs, d_out, d_status, d_chist);
     uint32_t st = 0;
     c->d2h(rec_offs, d_roffs, (nb + 1) * 8);
     c->d2h(&st, d_status, 4);

@@ -37,6 +37,20 @@ __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t x)
     }
     return x;
 }
+// Wave-wide totals (every lane gets the sum).
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x)
 {
     const uint32_t l = lane_id();

@@ -71,36 +71,61 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
     if (t == 0) dcount[blockIdx.x] = (uint32_t)d;
 }
 
-// grid = nblocks, one wave each: sequential composition of the chunk recency lists.
+// grid = nblocks, one wave each: sequential composition of the chunk recency lists. The
+// recency lists (256 B per chunk) are fetched 32 chunks ahead into registers and parked in
+// LDS, so the sequential chain never waits on global memory.
+constexpr uint32_t kComposeBatch = 32;
+
 __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__ chunk_first,
                                                     const uint8_t *__restrict__ R, const uint32_t *__restrict__ dcount,
                                                     uint32_t *__restrict__ S)
 {
+    __shared__ uint32_t s_R[kComposeBatch][64];
+    __shared__ uint32_t s_d[kComposeBatch];
     __shared__ uint8_t s_S[256], s_flag[256];
     const uint32_t b = blockIdx.x, l = threadIdx.x;
+    const uint32_t c0 = chunk_first[b], c1 = chunk_first[b + 1];
+    const uint32_t *R32 = (const uint32_t *)R;
     uint32_t st[4];
     for (int k = 0; k < 4; ++k) st[k] = 4 * l + k;
-    for (uint32_t c = chunk_first[b]; c < chunk_first[b + 1]; ++c) {
-        S[(size_t)c * 64 + l] = st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
-        const uint32_t d = dcount[c];
-        const uint8_t *Rc = R + (size_t)c * 256;
-        for (int k = 0; k < 4; ++k) s_flag[4 * l + k] = 0;
+    uint32_t pre[kComposeBatch], pred = 0;
+    auto fetch = [&](uint32_t cb) {
+#pragma unroll
+        for (uint32_t j = 0; j < kComposeBatch; ++j)
+            pre[j] = cb + j < c1 ? R32[(size_t)(cb + j) * 64 + l] : 0u;
+        pred = (l < kComposeBatch && cb + l < c1) ? dcount[cb + l] : 0u;
+    };
+    fetch(c0);
+    for (uint32_t cb = c0; cb < c1; cb += kComposeBatch) {
         __syncthreads();
-        for (uint32_t j = l; j < d; j += 64) s_flag[Rc[j]] = 1;
+#pragma unroll
+        for (uint32_t j = 0; j < kComposeBatch; ++j) s_R[j][l] = pre[j];
+        if (l < kComposeBatch) s_d[l] = pred;
         __syncthreads();
-        uint32_t keep[4], cnt = 0;
-        for (int k = 0; k < 4; ++k) {
-            keep[k] = s_flag[st[k]] == 0;
-            cnt += keep[k];
+        if (cb + kComposeBatch < c1) fetch(cb + kComposeBatch);
+        const uint32_t ce = min(c1, cb + kComposeBatch);
+        for (uint32_t c = cb; c < ce; ++c) {
+            S[(size_t)c * 64 + l] = st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
+            const uint32_t d = s_d[c - cb], rw = s_R[c - cb][l];
+            *(uint32_t *)&s_flag[4 * l] = 0;
+            __syncthreads();
+            for (uint32_t k = 0; k < 4; ++k)
+                if (4 * l + k < d) s_flag[(rw >> (8 * k)) & 255u] = 1;
+            __syncthreads();
+            uint32_t keep[4], cnt = 0;
+            for (int k = 0; k < 4; ++k) {
+                keep[k] = s_flag[st[k]] == 0;
+                cnt += keep[k];
+            }
+            uint32_t pos = d + wave_incl_sum(cnt) - cnt;
+            for (int k = 0; k < 4; ++k)
+                if (keep[k]) s_S[pos++] = (uint8_t)st[k];
+            for (uint32_t k = 0; k < 4; ++k)
+                if (4 * l + k < d) s_S[4 * l + k] = (uint8_t)(rw >> (8 * k));
+            __syncthreads();
+            for (int k = 0; k < 4; ++k) st[k] = s_S[4 * l + k];
+            __syncthreads();
         }
-        uint32_t pos = d + wave_incl_sum(cnt) - cnt;
-        __syncthreads();
-        for (int k = 0; k < 4; ++k)
-            if (keep[k]) s_S[pos++] = (uint8_t)st[k];
-        for (uint32_t j = l; j < d; j += 64) s_S[j] = Rc[j];
-        __syncthreads();
-        for (int k = 0; k < 4; ++k) st[k] = s_S[4 * l + k];
-        __syncthreads();
     }
 }
 
@@ -215,23 +240,44 @@ struct HChunk {
     uint32_t block, start, len, rel;
 };
 
-// freq + first occurrence of each MTF value, per block (huffman() main.cpp:231-244).
+// freq + first occurrence of each MTF value, per block (huffman() main.cpp:231-244), and the
+// histogram of every 4 K-symbol pack chunk (u16; the pack sizes its chunks from these
+// instead of re-reading the MTF stream). One workgroup per 64 K symbols of a block.
 __global__ __launch_bounds__(256) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
-                                                  uint32_t *__restrict__ freq, uint32_t *__restrict__ first)
+                                                  const uint32_t *__restrict__ pfirst, uint32_t *__restrict__ freq,
+                                                  uint32_t *__restrict__ first, uint16_t *__restrict__ chist)
 {
     __shared__ uint32_t h[4][256], f[256];
     const HChunk ch = chunks[blockIdx.x];
     const uint32_t t = threadIdx.x, w = t >> 6;
-    for (int k = 0; k < 4; ++k) h[k][t] = 0;
     f[t] = 0xffffffffu;
-    __syncthreads();
-    for (uint32_t i = t; i < ch.len; i += 256) {
-        const uint32_t v = in[ch.start + i];
-        atomicAdd(&h[w][v], 1u);
-        if (ch.rel + i < f[v]) atomicMin(&f[v], ch.rel + i);  // racy read only skips non-minima
+    uint32_t tot = 0;
+    for (uint32_t s0 = 0; s0 < ch.len; s0 += kPackChunkSyms) {
+        for (int k = 0; k < 4; ++k) h[k][t] = 0;
+        __syncthreads();
+        const uint32_t len = min(kPackChunkSyms, ch.len - s0), a = ch.start + s0;
+        if (len == kPackChunkSyms && (a & 15u) == 0) {
+            const uint4 v4 = *(const uint4 *)(in + a + 16 * t);
+            const uint32_t *vw = &v4.x;
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint32_t v = (vw[k >> 2] >> (8 * (k & 3))) & 255u, pos = ch.rel + s0 + 16 * t + k;
+                atomicAdd(&h[w][v], 1u);
+                if (pos < f[v]) atomicMin(&f[v], pos);  // racy read only skips non-minima
+            }
+        } else {
+            for (uint32_t i = t; i < len; i += 256) {
+                const uint32_t v = in[a + i], pos = ch.rel + s0 + i;
+                atomicAdd(&h[w][v], 1u);
+                if (pos < f[v]) atomicMin(&f[v], pos);
+            }
+        }
+        __syncthreads();
+        const uint32_t c = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        tot += c;
+        chist[(size_t)(pfirst[ch.block] + ((ch.rel + s0) / kPackChunkSyms)) * 256 + t] = (uint16_t)c;
+        __syncthreads();
     }
-    __syncthreads();
-    const uint32_t tot = h[0][t] + h[1][t] + h[2][t] + h[3][t];
     if (tot) {
         atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
         atomicMin(&first[(size_t)ch.block * 256 + t], f[t]);
@@ -251,7 +297,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     const uint32_t nb = bt.nblocks;
     std::vector<MChunk> hc;
     std::vector<HChunk> hh;
-    std::vector<uint32_t> cfirst(nb + 1);
+    std::vector<uint32_t> cfirst(nb + 1), pfirst(nb + 1);
+    pack_chunk_first(bt, pfirst.data());
     for (uint32_t b = 0; b < nb; ++b) {
         cfirst[b] = (uint32_t)hc.size();
         const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
@@ -274,14 +321,17 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     }
     cfirst[nb] = (uint32_t)hc.size();
     const uint32_t nch = (uint32_t)hc.size(), nhh = (uint32_t)hh.size();
-    const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + (nb + 1) * 4;
+    const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
     uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + 64);
     MChunk *d_chunks = (MChunk *)d_tab;
     HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
     uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));
+    uint32_t *d_pfirst = d_cfirst + (nb + 1);
     c->h2d(d_chunks, hc.data(), nch * sizeof(MChunk));
     c->h2d(d_hh, hh.data(), nhh * sizeof(HChunk));
     c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
+    c->h2d(d_pfirst, pfirst.data(), (nb + 1) * 4);
+    uint16_t *d_chist = (uint16_t *)c->get(WS_PACK_HIST, (size_t)pfirst[nb] * 256 * 2 + 64);
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
     uint32_t *d_S = (uint32_t *)c->get(WS_MTF_S, (size_t)nch * 256);
@@ -293,7 +343,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, nch, 256, 0, d_L, d_chunks, d_R, d_dcount);
     BMH_LAUNCH(c, "mtf_compose", k_mtf_compose, nb, 64, 0, d_cfirst, d_R, d_dcount, d_S);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
-    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_freq, d_first);
+    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_pfirst, d_freq, d_first, d_chist);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     if (h_freq32 || h_first32) c->sync();

@@ -21,7 +21,7 @@ namespace bmh {
 
 namespace {
 
-constexpr uint32_t kPackChunk = 4096;  // symbols per workgroup (256 threads x 16)
+constexpr uint32_t kPackChunk = kPackChunkSyms;  // symbols per workgroup (256 threads x 16)
 constexpr uint32_t kPackIPT = kPackChunk / 256;
 
 struct PChunk {
@@ -41,6 +41,22 @@ __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ m
     uint64_t total;
     block_excl_sum64<256>(s, s_tmp, &total);
     if (threadIdx.x == 0) cbits[blockIdx.x] = total;
+}
+
+// Chunk bit counts from the per-chunk MTF histograms: one wave per chunk, sum cnt[v] * len[v].
+__global__ __launch_bounds__(256) void k_pack_bits_hist(const uint16_t *__restrict__ chist,
+                                                        const PChunk *__restrict__ chunks, uint32_t nch,
+                                                        const DevTable *__restrict__ tabs, uint64_t *__restrict__ cbits)
+{
+    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63u;
+    if (c >= nch) return;
+    const DevTable *t = &tabs[chunks[c].block];
+    const uint2 h = *(const uint2 *)(chist + (size_t)c * 256 + 4 * l);
+    const uint32_t lw = *(const uint32_t *)(t->len + 4 * l);
+    uint64_t s = (uint64_t)(h.x & 0xffffu) * (lw & 255u) + (uint64_t)(h.x >> 16) * ((lw >> 8) & 255u) +
+                 (uint64_t)(h.y & 0xffffu) * ((lw >> 16) & 255u) + (uint64_t)(h.y >> 16) * (lw >> 24);
+    s = wave_sum64(s);
+    if (l == 0) cbits[c] = s;
 }
 
 // grid = nblocks; exclusive scan of the block's chunk bit counts (in place)
@@ -83,10 +99,20 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     uint8_t sym[kPackIPT];
     uint64_t mybits = 0;
     const uint32_t i0 = threadIdx.x * kPackIPT;
-    for (uint32_t k = 0; k < kPackIPT; ++k) {
-        const uint32_t i = i0 + k;
-        sym[k] = i < ch.len ? mtf[ch.start + i] : 0;
-        mybits += i < ch.len ? s_len[sym[k]] : 0u;
+    if (i0 + kPackIPT <= ch.len && ((ch.start + i0) & 15u) == 0) {
+        const uint4 v4 = *(const uint4 *)(mtf + ch.start + i0);
+        const uint32_t *vw = &v4.x;
+#pragma unroll
+        for (uint32_t k = 0; k < kPackIPT; ++k) {
+            sym[k] = (uint8_t)(vw[k >> 2] >> (8 * (k & 3)));
+            mybits += s_len[sym[k]];
+        }
+    } else {
+        for (uint32_t k = 0; k < kPackIPT; ++k) {
+            const uint32_t i = i0 + k;
+            sym[k] = i < ch.len ? mtf[ch.start + i] : 0;
+            mybits += i < ch.len ? s_len[sym[k]] : 0u;
+        }
     }
     uint64_t total;
     uint64_t tb = block_excl_sum64<256>(mybits, s_tmp, &total) + sh0;
@@ -103,18 +129,34 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     const uint32_t nwords = (uint32_t)((own_end - W0 * 32 + 31) >> 5);
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) s_img[w] = 0;
     __syncthreads();
-    for (uint32_t k = 0; k < kPackIPT; ++k) {
-        if (i0 + k >= ch.len) break;
-        uint32_t l = s_len[sym[k]];
-        const uint64_t code = s_code[sym[k]];
-        while (l > 0) {
-            const uint32_t off = (uint32_t)(tb & 31u);
-            const uint32_t take = min(l, 32u - off);
-            const uint32_t bits = (uint32_t)((code >> (l - take)) & ((take == 32) ? 0xffffffffull : ((1ull << take) - 1)));
-            atomicOr(&s_img[tb >> 5], bits << (32u - off - take));
-            tb += take;
-            l -= take;
+    {
+        // this thread's bits [tb, tb + mybits) of the image, accumulated MSB-first in a 64-bit
+        // register and flushed a word at a time: words wholly inside the range are stored,
+        // the first / last partial words are shared with the neighbours (LDS atomicOr)
+        uint32_t w = (uint32_t)(tb >> 5), nacc = (uint32_t)(tb & 31u);
+        const bool head_shared = nacc != 0;
+        uint64_t acc = 0;
+        for (uint32_t k = 0; k < kPackIPT; ++k) {
+            if (i0 + k >= ch.len) break;
+            uint32_t l = s_len[sym[k]];
+            const uint64_t code = s_code[sym[k]];
+            while (l > 0) {
+                const uint32_t take = min(l, 32u);
+                const uint64_t piece = (code >> (l - take)) & ((1ull << take) - 1);
+                acc |= piece << (64 - nacc - take);
+                nacc += take;
+                l -= take;
+                if (nacc >= 32) {
+                    const uint32_t word = (uint32_t)(acc >> 32);
+                    if (w == (uint32_t)(tb >> 5) && head_shared) atomicOr(&s_img[w], word);
+                    else s_img[w] = word;
+                    ++w;
+                    acc <<= 32;
+                    nacc -= 32;
+                }
+            }
         }
+        if (nacc) atomicOr(&s_img[w], (uint32_t)(acc >> 32));
     }
     __syncthreads();
     // words wholly inside [G, own_end) are stored; the edge words are shared with the
@@ -198,7 +240,7 @@ void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_f
 }
 
 void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
-                    uint8_t *d_out, const uint32_t *d_status)
+                    uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist)
 {
     if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const uint32_t nb = bt.nblocks;
@@ -224,7 +266,10 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
     uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
     c->h2d(d_chunks, hc.data(), nch * sizeof(PChunk));
     c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
-    BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits);
+    if (d_chist)
+        BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(nch, 4), 256, 0, d_chist, d_chunks, nch, d_tabs, d_cbits);
+    else
+        BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits);
     BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
     BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits, d_pay_offs, d_cfirst,
                (uint32_t *)d_out, d_status);
@@ -245,7 +290,7 @@ void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_ta
     uint64_t *d_pay = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 1) * 8 + 64);
     c->h2d(d_tab, ht.data(), nb * sizeof(DevTable));
     c->h2d(d_pay, pay_offs, nb * 8);
-    pack_batch_dev(c, d_mtf, bt, d_tab, d_pay, d_out, nullptr);
+    pack_batch_dev(c, d_mtf, bt, d_tab, d_pay, d_out, nullptr, nullptr);
     c->sync();
 }
 
