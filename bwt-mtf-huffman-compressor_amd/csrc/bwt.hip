@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
 // so the keys cost no global gathers; the dense finish pass reads them coalesced.
 __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *__restrict__ chunks,
                                                      const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk,
-                                                     uint64_t *__restrict__ key8)
+                                                     uint3 *__restrict__ rec)
 {
     __shared__ uint16_t s_ent[kG1Chunk];  // chunk-relative position
     // byte j <-> block position start - 4 + j (cyclic), j < len + 12
@@ -310,9 +310,12 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint64_t key = __builtin_bswap64((v64 >> 16) | (b8 << 48)) | (v64 & 255u);
         const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
         const uint32_t slot = s_off[d] + (i - s_ls[d]);
-        a.sa[boff + slot] = p;
-        key8[boff + slot] = key;
-        if (s_blen[d] == 1) {
+        const uint32_t blen = s_blen[d];
+        if (blen >= 2 && blen <= kDenseCap)  // the dense finish reads {p, key}, writes SA
+            rec[boff + slot] = make_uint3(p, (uint32_t)key, (uint32_t)(key >> 32));
+        else
+            a.sa[boff + slot] = p;
+        if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
             if (p == 0) a.prim[b] = slot;
         }
@@ -353,7 +356,7 @@ __device__ __forceinline__ uint32_t bm_head_gt(const uint32_t *bm, uint32_t i, u
 
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
-                                                   const uint2 *__restrict__ bk, const uint64_t *__restrict__ key8,
+                                                   const uint2 *__restrict__ bk, const uint3 *__restrict__ rec,
                                                    uint32_t lo, int dense)
 {
     constexpr uint32_t IPT = (CAP + NT - 1) / NT;
@@ -395,13 +398,16 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     for (uint32_t k = 0; k < IPT; ++k) {
         const uint32_t e = t + k * NT;
         if (e < len) {
-            const uint32_t p = a.sa[gstart + e];
+            uint32_t p;
             uint64_t w;
             if (dense) {
-                const uint64_t key = key8[gstart + e];
+                const uint3 r = rec[gstart + e];
+                p = r.x;
+                const uint64_t key = ((uint64_t)r.z << 32) | r.y;
                 w = key << (kG1Bits - 8);
                 pv[k] = packL ? (p << 8) | (uint32_t)(key & 255u) : p;
             } else {
+                p = a.sa[gstart + e];
                 w = rot_window(blk, n, p, db);
                 pv[k] = p;
             }
@@ -1129,7 +1135,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
-    uint64_t *key8 = (uint64_t *)c->get(WS_KEY8, N * 8);
+    uint3 *rec = (uint3 *)c->get(WS_KEY8, N * 12);
     uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
@@ -1167,12 +1173,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
     BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, fin_cur, big,
                d_cnt);
-    BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, key8);
+    BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
     // the dense finish appends deferred segments after the global pass's list entries
     da.fin_next = fin_cur;
     da.big_next = big2;
     BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_seg<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
-               da, nullptr, bk, key8, 0u, 1);
+               da, nullptr, bk, rec, 0u, 1);
     read_counters();
     uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
     Seg4 *big_cur = big, *big_nxt = big2;
