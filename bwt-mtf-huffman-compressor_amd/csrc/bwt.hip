@@ -37,7 +37,6 @@ constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass wor
 constexpr uint32_t kG1Bits = 10;                // global-pass digit: first byte + 2 bits
 constexpr uint32_t kG1Bins = 1u << kG1Bits;
 constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passes
-constexpr uint32_t kSegKeyBits = kSegDigit + 32;  // bits one finish pass resolves
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
 constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kFinNT = 256, kFinCap = 4096;
@@ -143,6 +142,13 @@ __device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, ui
     }
 }
 
+// Compact rotation record the global pass writes for dense buckets (u64): rotation bits
+// [kG1Bits, kG1Bits + 12 + R) | p (P bits) | last-column byte, with P = bits of the block's
+// largest position and R = min(32, 44 - P) (4 MiB blocks: P = 22, R = 22, so one dense
+// finish resolves rotation bits up to 44; rarer deeper ties go to list passes).
+__device__ __forceinline__ uint32_t rec_pbits(uint32_t n) { return n <= 2 ? 1u : 32u - (uint32_t)__builtin_clz(n - 1); }
+__device__ __forceinline__ uint32_t rec_rbits(uint32_t P) { return min(32u, 44u - P); }
+
 // ------------------------------------------------------------------------- global pass
 // Counting sort of every block by its first kG1Bits rotation bits. Chunks of <= 16 K
 // positions whose batch boundaries are 16-byte multiples (a block's first chunk takes the
@@ -233,7 +239,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
 // so the keys cost no global gathers; the dense finish pass reads them coalesced.
 __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *__restrict__ chunks,
                                                      const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk,
-                                                     uint3 *__restrict__ rec)
+                                                     uint64_t *__restrict__ rec)
 {
     __shared__ uint16_t s_ent[kG1Chunk];  // chunk-relative position
     // byte j <-> block position start - 4 + j (cyclic), j < len + 12
@@ -311,9 +317,11 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
         const uint32_t slot = s_off[d] + (i - s_ls[d]);
         const uint32_t blen = s_blen[d];
-        if (blen >= 2 && blen <= kDenseCap)  // the dense finish reads {p, key}, writes SA
-            rec[boff + slot] = make_uint3(p, (uint32_t)key, (uint32_t)(key >> 32));
-        else
+        if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
+            const uint32_t P = rec_pbits(n), R = rec_rbits(P);
+            const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
+            rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
+        } else
             a.sa[boff + slot] = p;
         if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
@@ -356,7 +364,7 @@ __device__ __forceinline__ uint32_t bm_head_gt(const uint32_t *bm, uint32_t i, u
 
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
-                                                   const uint2 *__restrict__ bk, const uint3 *__restrict__ rec,
+                                                   const uint2 *__restrict__ bk, const uint64_t *__restrict__ rec,
                                                    uint32_t lo, int dense)
 {
     constexpr uint32_t IPT = (CAP + NT - 1) / NT;
@@ -393,26 +401,26 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     // dense: the last-column byte rides in s_pos when positions fit 24 bits; otherwise (and
     // for list segments) it is gathered at the end
     const bool packL = dense && n <= (1u << 24);
+    const uint32_t P = rec_pbits(n), R = dense ? rec_rbits(P) : 32u;
     uint32_t pv[IPT], dv[IPT], rv[IPT];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         const uint32_t e = t + k * NT;
         if (e < len) {
-            uint32_t p;
-            uint64_t w;
             if (dense) {
-                const uint3 r = rec[gstart + e];
-                p = r.x;
-                const uint64_t key = ((uint64_t)r.z << 32) | r.y;
-                w = key << (kG1Bits - 8);
-                pv[k] = packL ? (p << 8) | (uint32_t)(key & 255u) : p;
+                const uint64_t r = rec[gstart + e];
+                const uint64_t sub = r >> (P + 8);
+                const uint32_t p = (uint32_t)(r >> 8) & (uint32_t)((1ull << P) - 1);
+                dv[k] = (uint32_t)(sub >> R);
+                rv[k] = (uint32_t)(sub & ((1ull << R) - 1));
+                pv[k] = packL ? (p << 8) | (uint32_t)(r & 255u) : p;
             } else {
-                p = a.sa[gstart + e];
-                w = rot_window(blk, n, p, db);
+                const uint32_t p = a.sa[gstart + e];
+                const uint64_t w = rot_window(blk, n, p, db);
                 pv[k] = p;
+                dv[k] = (uint32_t)(w >> (64 - kSegDigit));
+                rv[k] = (uint32_t)(w >> (32 - kSegDigit));
             }
-            dv[k] = (uint32_t)(w >> (64 - kSegDigit));
-            rv[k] = (uint32_t)(w >> (32 - kSegDigit));
             atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
         }
     }
@@ -447,7 +455,7 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         }
     }
     __syncthreads();
-    const uint64_t newbits = (uint64_t)db + kSegKeyBits;
+    const uint64_t newbits = (uint64_t)db + kSegDigit + R;
     const bool final_depth = newbits >= 8ull * n;
     // rank every element inside its sub-bucket; last-column gathers and stores afterwards
     uint32_t sl[IPT], lb[IPT];
@@ -475,11 +483,7 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
             }
             const uint32_t slot = gstart + s0 + lt + eqb;
             const uint32_t gs = gstart + s0 + lt;
-            if (eqt > 1 && eqb == 0) {
-                a.groups[atomicAdd(&a.cnt->dgroups, 1u)] =
-                    make_uint4(gs, eqt, (uint32_t)newbits, b | (final_depth ? kFinalFlag : 0u));
-                if (!final_depth) a.bflag[b] = 1;
-            }
+            if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)newbits, b, n);  // tied so far
             a.sa[slot] = p;
             if (eqt == 1 || final_depth) {
                 sl[k] = slot;
@@ -1135,7 +1139,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
-    uint3 *rec = (uint3 *)c->get(WS_KEY8, N * 12);
+    uint64_t *rec = (uint64_t *)c->get(WS_KEY8, N * 8);
     uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
