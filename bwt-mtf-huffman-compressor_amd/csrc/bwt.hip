@@ -37,6 +37,7 @@ constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass wor
 constexpr uint32_t kG1Bits = 10;                // global-pass digit: first byte + 2 bits
 constexpr uint32_t kG1Bins = 1u << kG1Bits;
 constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passes
+constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
 constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kFinNT = 256, kFinCap = 4096;
@@ -331,36 +332,15 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
 }
 
 // ------------------------------------------------------------------------- finish pass
-// One workgroup of NT threads sorts one segment of <= CAP tied rotations (equal in bits
-// [0, db)). dense = 1: the buckets of the global pass (db = kG1Bits), XCD-aware: workgroup
-// i -> lane i % 8 -> blocks b = lane mod 8, keys read coalesced from key8. dense = 0: the
+// One workgroup of NT threads sorts one segment of <= CAP rotations that are equal in bits
+// [0, db). dense = 1: the buckets of the global pass (db = kG1Bits), XCD-aware: workgroup
+// i -> lane i % 8 -> blocks b = lane mod 8, compact records read coalesced. dense = 0: the
 // list entries with lo < len <= CAP, rotation windows gathered from the text.
-// LDS counting sort by the next 12 bits, then every element (one lane each, consecutive
-// elements in a wave) ranks itself inside its sub-bucket by the next 32 bits (bit depth
-// db + 44). Sub-bucket bounds come from a head bitmap; sub-buckets > kSmallM are deferred.
-// 12-bit counters are packed two per word (16-bit halves; segments < 65536).
-__device__ __forceinline__ uint32_t bm_head_le(const uint32_t *bm, uint32_t i)
-{
-    // highest set bit <= i (bit 0 is always set)
-    uint32_t w = i >> 5;
-    uint32_t bits = bm[w] & (0xffffffffu >> (31 - (i & 31u)));
-    while (!bits) bits = bm[--w];
-    return w * 32 + 31 - __builtin_clz(bits);
-}
-
-__device__ __forceinline__ uint32_t bm_head_gt(const uint32_t *bm, uint32_t i, uint32_t len)
-{
-    // lowest set bit > i, or len
-    uint32_t w = i >> 5;
-    const uint32_t sh = (i & 31u) + 1;
-    uint32_t bits = sh == 32 ? 0u : bm[w] & (0xffffffffu << sh);
-    const uint32_t wend = (len + 31) >> 5;
-    while (!bits) {
-        if (++w >= wend) return len;
-        bits = bm[w];
-    }
-    return min(len, w * 32 + (uint32_t)__builtin_ctz(bits));
-}
+// Each thread keeps its elements (position, last-column byte, next 12-bit digit, next R-bit
+// rest) in registers; LDS holds only the rests and the 12-bit counters (packed two per
+// word, 16-bit halves). Counting sort by the digit, then every element ranks itself inside
+// its sub-bucket (bounds = neighbouring counters) by the rest: bit depth db + 12 + R.
+// Sub-buckets > kSmallM, and rotations still tied, are deferred to list passes.
 
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
@@ -370,9 +350,8 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     constexpr uint32_t IPT = (CAP + NT - 1) / NT;
     constexpr uint32_t NDIG = 1u << kSegDigit, WPT = NDIG / 2 / NT;  // counter words per thread
     static_assert(CAP < 65536 && WPT >= 1 && NDIG / 2 == WPT * NT, "finish shape");
-    __shared__ uint32_t s_pos[CAP], s_rest[CAP];
+    __shared__ uint32_t s_rest[CAP];
     __shared__ uint32_t s_cnt[NDIG / 2];
-    __shared__ uint32_t s_bm[CAP / 32 + 2];
     __shared__ uint32_t s_tmp[NT / 64 + 1];
     uint32_t gstart, len, db, b;
     if (dense) {
@@ -396,13 +375,12 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     const uint8_t *blk = a.data + boff;
     const uint32_t t = threadIdx.x;
     for (uint32_t i = t; i < NDIG / 2; i += NT) s_cnt[i] = 0;
-    for (uint32_t i = t; i < CAP / 32 + 2; i += NT) s_bm[i] = 0;
     __syncthreads();
-    // dense: the last-column byte rides in s_pos when positions fit 24 bits; otherwise (and
-    // for list segments) it is gathered at the end
-    const bool packL = dense && n <= (1u << 24);
     const uint32_t P = rec_pbits(n), R = dense ? rec_rbits(P) : 32u;
-    uint32_t pv[IPT], dv[IPT], rv[IPT];
+    // registers per element: pl = position (<< 8 | last-column byte when packL), rv = rest,
+    // dd = digit | LDS slot << 12 (the slot is filled in by the scatter)
+    const bool packL = dense && P <= 24;
+    uint32_t pl[IPT], dd[IPT], rv[IPT];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         const uint32_t e = t + k * NT;
@@ -411,22 +389,22 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
                 const uint64_t r = rec[gstart + e];
                 const uint64_t sub = r >> (P + 8);
                 const uint32_t p = (uint32_t)(r >> 8) & (uint32_t)((1ull << P) - 1);
-                dv[k] = (uint32_t)(sub >> R);
+                pl[k] = packL ? (p << 8) | ((uint32_t)r & 255u) : p;
+                dd[k] = (uint32_t)(sub >> R);
                 rv[k] = (uint32_t)(sub & ((1ull << R) - 1));
-                pv[k] = packL ? (p << 8) | (uint32_t)(r & 255u) : p;
             } else {
                 const uint32_t p = a.sa[gstart + e];
                 const uint64_t w = rot_window(blk, n, p, db);
-                pv[k] = p;
-                dv[k] = (uint32_t)(w >> (64 - kSegDigit));
+                pl[k] = p;
+                dd[k] = (uint32_t)(w >> (64 - kSegDigit));
                 rv[k] = (uint32_t)(w >> (32 - kSegDigit));
             }
-            atomicAdd(&s_cnt[dv[k] >> 1], 1u << (16 * (dv[k] & 1u)));
+            atomicAdd(&s_cnt[dd[k] >> 1], 1u << (16 * (dd[k] & 1u)));
         }
     }
     __syncthreads();
     {
-        // thread t owns counter words WPT*t .. WPT*t + WPT - 1; marks the sub-bucket heads
+        // thread t owns counter words WPT*t .. WPT*t + WPT - 1: counts -> starts
         uint32_t c[2 * WPT], sum = 0;
         for (uint32_t j = 0; j < WPT; ++j) {
             const uint32_t w = s_cnt[WPT * t + j];
@@ -437,8 +415,6 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         uint32_t ex = block_excl_sum<NT>(sum, s_tmp, nullptr);
         for (uint32_t j = 0; j < WPT; ++j) {
             const uint32_t e0 = ex, e1 = ex + c[2 * j];
-            if (c[2 * j]) atomicOr(&s_bm[e0 >> 5], 1u << (e0 & 31u));
-            if (c[2 * j + 1]) atomicOr(&s_bm[e1 >> 5], 1u << (e1 & 31u));
             s_cnt[WPT * t + j] = e0 | (e1 << 16);
             ex = e1 + c[2 * j + 1];
         }
@@ -448,55 +424,75 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     for (uint32_t k = 0; k < IPT; ++k) {
         const uint32_t e = t + k * NT;
         if (e < len) {
-            const uint32_t sh = 16 * (dv[k] & 1u);
-            const uint32_t dst = (atomicAdd(&s_cnt[dv[k] >> 1], 1u << sh) >> sh) & 0xffffu;
-            s_pos[dst] = pv[k];
-            s_rest[dst] = rv[k];
+            const uint32_t d = dd[k], sh = 16 * (d & 1u);
+            const uint32_t me = (atomicAdd(&s_cnt[d >> 1], 1u << sh) >> sh) & 0xffffu;
+            s_rest[me] = rv[k];
+            dd[k] = d | (me << kSegDigit);
         }
     }
     __syncthreads();
+    // s_cnt now holds every sub-bucket's end; its start is the previous digit's end
     const uint64_t newbits = (uint64_t)db + kSegDigit + R;
     const bool final_depth = newbits >= 8ull * n;
-    // rank every element inside its sub-bucket; last-column gathers and stores afterwards
-    uint32_t sl[IPT], lb[IPT];
+    // rank in registers; outputs are parked in LDS at their segment slot (s_rest is free
+    // again after the next barrier) and stored in slot order, coalesced
+    uint32_t out[IPT];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         const uint32_t e = t + k * NT;
-        sl[k] = 0xffffffffu;
-        if (e < len) {
-            const uint32_t s0 = bm_head_le(s_bm, e), s1 = bm_head_gt(s_bm, e, len), m = s1 - s0;
-            const uint32_t pe = s_pos[e], p = packL ? pe >> 8 : pe;
-            pv[k] = pe;
-            if (m > kSmallM) {
-                a.sa[gstart + e] = p;  // deferred, grouped by the 12-bit digit
-                if (e == s0) defer_segment(a, gstart + s0, m, db + kSegDigit, b, n);
-                continue;
-            }
-            const uint32_t r = s_rest[e];
-            uint32_t lt = 0, eqb = 0, eqt = 0;
+        out[k] = 0xffffffffu;
+        if (e >= len) continue;
+        const uint32_t d = dd[k] & (kSegDigits1 - 1), me = dd[k] >> kSegDigit;
+        const uint32_t p = packL ? pl[k] >> 8 : pl[k];
+        const uint32_t s1 = (s_cnt[d >> 1] >> (16 * (d & 1u))) & 0xffffu;
+        const uint32_t s0 = d ? (s_cnt[(d - 1) >> 1] >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
+        const uint32_t m = s1 - s0;
+        if (m > kSmallM) {
+            out[k] = me;  // deferred, grouped by the 12-bit digit
+            if (me == s0) defer_segment(a, gstart + s0, m, db + kSegDigit, b, n);
+            continue;
+        }
+        uint32_t lt = 0, eqb = 0, eqt = 1;
+        if (m > 1) {
+            const uint32_t r = rv[k];
+            eqt = 0;
             for (uint32_t f = s0; f < s1; ++f) {
                 const uint32_t rf = s_rest[f];
                 lt += rf < r;
                 const bool eq = rf == r;
                 eqt += eq;
-                eqb += eq && f < e;
-            }
-            const uint32_t slot = gstart + s0 + lt + eqb;
-            const uint32_t gs = gstart + s0 + lt;
-            if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)newbits, b, n);  // tied so far
-            a.sa[slot] = p;
-            if (eqt == 1 || final_depth) {
-                sl[k] = slot;
-                if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+                eqb += eq && f < me;
             }
         }
+        const uint32_t local = s0 + lt + eqb, gs = gstart + s0 + lt;
+        if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)newbits, b, n);  // tied so far
+        out[k] = local;
+        if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = (eqt == 1 ? gstart + local : gs) - boff;
     }
+    __syncthreads();
+    if (packL) {
+        // slot -> (position << 8 | last-column byte); a slot whose rotation is not final yet
+        // gets its L rewritten when a later pass resolves it
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k)
-        if (sl[k] != 0xffffffffu) lb[k] = packL ? pv[k] & 255u : lastcol_byte(blk, n, pv[k]);
+        for (uint32_t k = 0; k < IPT; ++k)
+            if (out[k] != 0xffffffffu) s_rest[out[k]] = pl[k];
+        __syncthreads();
+        for (uint32_t i = t; i < len; i += NT) {
+            const uint32_t v = s_rest[i];
+            a.sa[gstart + i] = v >> 8;
+            a.L[gstart + i] = (uint8_t)v;
+        }
+    } else {
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k)
-        if (sl[k] != 0xffffffffu) a.L[sl[k]] = (uint8_t)lb[k];
+        for (uint32_t k = 0; k < IPT; ++k)
+            if (out[k] != 0xffffffffu) s_rest[out[k]] = pl[k];
+        __syncthreads();
+        for (uint32_t i = t; i < len; i += NT) {
+            const uint32_t p = s_rest[i];
+            a.sa[gstart + i] = p;
+            a.L[gstart + i] = lastcol_byte(blk, n, p);
+        }
+    }
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
