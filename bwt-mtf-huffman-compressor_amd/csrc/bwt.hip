@@ -343,65 +343,29 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
 // Sub-buckets > kSmallM, and rotations still tied, are deferred to list passes.
 
 template <uint32_t NT, uint32_t CAP>
-__global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
-                                                   const uint2 *__restrict__ bk, const uint64_t *__restrict__ rec,
-                                                   uint32_t lo, int dense)
-{
-    constexpr uint32_t IPT = (CAP + NT - 1) / NT;
-    constexpr uint32_t NDIG = 1u << kSegDigit, WPT = NDIG / 2 / NT;  // counter words per thread
+struct FinishShape {
+    static constexpr uint32_t IPT = (CAP + NT - 1) / NT;
+    static constexpr uint32_t NDIG = 1u << kSegDigit, WPT = NDIG / 2 / NT;  // counter words per thread
     static_assert(CAP < 65536 && WPT >= 1 && NDIG / 2 == WPT * NT, "finish shape");
-    __shared__ uint32_t s_rest[CAP];
-    __shared__ uint32_t s_cnt[NDIG / 2];
-    __shared__ uint32_t s_tmp[NT / 64 + 1];
-    uint32_t gstart, len, db, b;
-    if (dense) {
-        const uint32_t x = blockIdx.x & 7u, k = blockIdx.x >> 3;
-        b = x + 8u * (k >> kG1Bits);
-        if (b >= a.nb) return;
-        const uint2 e = bk[(size_t)b * kG1Bins + (k & (kG1Bins - 1))];
-        len = e.y;
-        if (len < 2 || len > CAP) return;
-        gstart = a.boffs[b] + e.x;
-        db = kG1Bits;
-    } else {
-        const Seg4 s = list[blockIdx.x];
-        gstart = s.x;
-        len = s.y;
-        db = s.z;
-        b = s.w;
-        if (len <= lo || len > CAP) return;
-    }
+};
+
+// The finish of one segment once every element is in registers: pl = position (<< 8 | last-
+// column byte when packL), dd = 12-bit digit, rv = R-bit rest. s_cnt must be zero on entry
+// and is zero again on return (ends with a barrier).
+template <uint32_t NT, uint32_t CAP>
+__device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, uint32_t len, uint32_t db, uint32_t b,
+                                            uint32_t R, bool packL, uint32_t (&pl)[FinishShape<NT, CAP>::IPT],
+                                            uint32_t (&dd)[FinishShape<NT, CAP>::IPT],
+                                            uint32_t (&rv)[FinishShape<NT, CAP>::IPT], uint32_t *s_rest,
+                                            uint32_t *s_cnt, uint32_t *s_tmp)
+{
+    constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT, WPT = FinishShape<NT, CAP>::WPT;
+    const uint32_t t = threadIdx.x;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < NDIG / 2; i += NT) s_cnt[i] = 0;
-    __syncthreads();
-    const uint32_t P = rec_pbits(n), R = dense ? rec_rbits(P) : 32u;
-    // registers per element: pl = position (<< 8 | last-column byte when packL), rv = rest,
-    // dd = digit | LDS slot << 12 (the slot is filled in by the scatter)
-    const bool packL = dense && P <= 24;
-    uint32_t pl[IPT], dd[IPT], rv[IPT];
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t e = t + k * NT;
-        if (e < len) {
-            if (dense) {
-                const uint64_t r = rec[gstart + e];
-                const uint64_t sub = r >> (P + 8);
-                const uint32_t p = (uint32_t)(r >> 8) & (uint32_t)((1ull << P) - 1);
-                pl[k] = packL ? (p << 8) | ((uint32_t)r & 255u) : p;
-                dd[k] = (uint32_t)(sub >> R);
-                rv[k] = (uint32_t)(sub & ((1ull << R) - 1));
-            } else {
-                const uint32_t p = a.sa[gstart + e];
-                const uint64_t w = rot_window(blk, n, p, db);
-                pl[k] = p;
-                dd[k] = (uint32_t)(w >> (64 - kSegDigit));
-                rv[k] = (uint32_t)(w >> (32 - kSegDigit));
-            }
-            atomicAdd(&s_cnt[dd[k] >> 1], 1u << (16 * (dd[k] & 1u)));
-        }
-    }
+    for (uint32_t k = 0; k < IPT; ++k)
+        if (t + k * NT < len) atomicAdd(&s_cnt[dd[k] >> 1], 1u << (16 * (dd[k] & 1u)));
     __syncthreads();
     {
         // thread t owns counter words WPT*t .. WPT*t + WPT - 1: counts -> starts
@@ -422,8 +386,7 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t e = t + k * NT;
-        if (e < len) {
+        if (t + k * NT < len) {
             const uint32_t d = dd[k], sh = 16 * (d & 1u);
             const uint32_t me = (atomicAdd(&s_cnt[d >> 1], 1u << sh) >> sh) & 0xffffu;
             s_rest[me] = rv[k];
@@ -431,24 +394,20 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         }
     }
     __syncthreads();
-    // s_cnt now holds every sub-bucket's end; its start is the previous digit's end
+    // s_cnt now holds every sub-bucket's end; its start is the previous digit's end. Rank in
+    // registers; outputs are parked in LDS at their segment slot and stored in slot order.
     const uint64_t newbits = (uint64_t)db + kSegDigit + R;
     const bool final_depth = newbits >= 8ull * n;
-    // rank in registers; outputs are parked in LDS at their segment slot (s_rest is free
-    // again after the next barrier) and stored in slot order, coalesced
-    uint32_t out[IPT];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t e = t + k * NT;
-        out[k] = 0xffffffffu;
-        if (e >= len) continue;
+        if (t + k * NT >= len) continue;
         const uint32_t d = dd[k] & (kSegDigits1 - 1), me = dd[k] >> kSegDigit;
         const uint32_t p = packL ? pl[k] >> 8 : pl[k];
         const uint32_t s1 = (s_cnt[d >> 1] >> (16 * (d & 1u))) & 0xffffu;
         const uint32_t s0 = d ? (s_cnt[(d - 1) >> 1] >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
         const uint32_t m = s1 - s0;
         if (m > kSmallM) {
-            out[k] = me;  // deferred, grouped by the 12-bit digit
+            dd[k] = me;  // deferred, grouped by the 12-bit digit
             if (me == s0) defer_segment(a, gstart + s0, m, db + kSegDigit, b, n);
             continue;
         }
@@ -466,33 +425,100 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         }
         const uint32_t local = s0 + lt + eqb, gs = gstart + s0 + lt;
         if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)newbits, b, n);  // tied so far
-        out[k] = local;
+        dd[k] = local;  // dd now holds the element's slot in the segment
         if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = (eqt == 1 ? gstart + local : gs) - boff;
     }
     __syncthreads();
-    if (packL) {
-        // slot -> (position << 8 | last-column byte); a slot whose rotation is not final yet
-        // gets its L rewritten when a later pass resolves it
+    // slot -> position (<< 8 | L); a slot whose rotation is not final yet gets its L
+    // rewritten when a later pass resolves it
 #pragma unroll
-        for (uint32_t k = 0; k < IPT; ++k)
-            if (out[k] != 0xffffffffu) s_rest[out[k]] = pl[k];
-        __syncthreads();
+    for (uint32_t k = 0; k < IPT; ++k)
+        if (t + k * NT < len) s_rest[dd[k]] = pl[k];
+    for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
+    __syncthreads();
+    if (packL) {
         for (uint32_t i = t; i < len; i += NT) {
             const uint32_t v = s_rest[i];
             a.sa[gstart + i] = v >> 8;
             a.L[gstart + i] = (uint8_t)v;
         }
     } else {
-#pragma unroll
-        for (uint32_t k = 0; k < IPT; ++k)
-            if (out[k] != 0xffffffffu) s_rest[out[k]] = pl[k];
-        __syncthreads();
         for (uint32_t i = t; i < len; i += NT) {
             const uint32_t p = s_rest[i];
             a.sa[gstart + i] = p;
             a.L[gstart + i] = lastcol_byte(blk, n, p);
         }
     }
+    __syncthreads();
+}
+
+// List segments (lo < len <= CAP) at any depth: rotation windows gathered from the text.
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
+{
+    constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT;
+    __shared__ uint32_t s_rest[CAP];
+    __shared__ uint32_t s_cnt[FinishShape<NT, CAP>::NDIG / 2];
+    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    const Seg4 sg = list[blockIdx.x];
+    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
+    if (len <= lo || len > CAP) return;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
+    uint32_t pl[IPT], dd[IPT], rv[IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        if (t + k * NT < len) {
+            const uint32_t p = a.sa[gstart + t + k * NT];
+            const uint64_t w = rot_window(blk, n, p, db);
+            pl[k] = p;
+            dd[k] = (uint32_t)(w >> (64 - kSegDigit));
+            rv[k] = (uint32_t)(w >> (32 - kSegDigit));
+        }
+    }
+    __syncthreads();
+    finish_core<NT, CAP>(a, gstart, len, db, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp);
+}
+
+// Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
+// XCD-aware: workgroup i -> lane i % 8 -> blocks b = lane mod 8. Compact records read
+// coalesced. (A persistent variant that prefetched the next bucket into registers measured
+// slower: the extra registers cost a workgroup per CU.)
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__restrict__ bk,
+                                                     const uint64_t *__restrict__ rec)
+{
+    constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT;
+    __shared__ uint32_t s_rest[CAP];
+    __shared__ uint32_t s_cnt[FinishShape<NT, CAP>::NDIG / 2];
+    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    const uint32_t x = blockIdx.x & 7u, kb = blockIdx.x >> 3;
+    const uint32_t b = x + 8u * (kb >> kG1Bits);
+    if (b >= a.nb) return;
+    const uint2 e = bk[(size_t)b * kG1Bins + (kb & (kG1Bins - 1))];
+    if (e.y < 2 || e.y > CAP) return;
+    const uint32_t t = threadIdx.x;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t P = rec_pbits(n), R = rec_rbits(P);
+    const bool packL = P <= 24;
+    for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
+    const uint64_t *r0 = rec + boff + e.x;
+    uint32_t pl[IPT], dd[IPT], rv[IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        if (t + k * NT < e.y) {
+            const uint64_t r = r0[t + k * NT];
+            const uint64_t sub = r >> (P + 8);
+            const uint32_t p = (uint32_t)(r >> 8) & (uint32_t)((1ull << P) - 1);
+            pl[k] = packL ? (p << 8) | ((uint32_t)r & 255u) : p;
+            dd[k] = (uint32_t)(sub >> R);
+            rv[k] = (uint32_t)(sub & ((1ull << R) - 1));
+        }
+    }
+    __syncthreads();
+    finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -1177,8 +1203,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // the dense finish appends deferred segments after the global pass's list entries
     da.fin_next = fin_cur;
     da.big_next = big2;
-    BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_seg<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
-               da, nullptr, bk, rec, 0u, 1);
+    BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
+               da, bk, rec);
     read_counters();
     uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
     Seg4 *big_cur = big, *big_nxt = big2;
@@ -1191,10 +1217,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         if (nfin > 0) {
             da.fin_next = fin_nxt;
             da.big_next = big_nxt;
-            BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, bk, nullptr,
-                       1u, 0);
-            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfin, kBigNT, 0, da, fin_cur, bk,
-                       nullptr, kFinCap, 0);
+            BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
+            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfin, kBigNT, 0, da, fin_cur, kFinCap);
         }
         if (nbig > 0) {
             hs.resize(nbig);
