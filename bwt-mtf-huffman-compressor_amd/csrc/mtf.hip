@@ -31,12 +31,14 @@ namespace {
 
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 constexpr int kLanes = 256;           // lanes (chunks) per encode workgroup
+constexpr int kMtfGroup = 2;          // symbols per batched MTF step
 
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
 };
 
-// grid = chunks; 256 threads. R[c][0..d) = distinct symbols, most recent last occurrence first.
+// grid = chunks; 256 threads x 16 symbols. R[c][0..d) = distinct symbols, most recent last
+// occurrence first.
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                      uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
 {
@@ -47,8 +49,21 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
     const uint32_t t = threadIdx.x;
     lastpos[t] = -1;
     if (t < kMtfChunk / 32) bset[t] = 0;
+    // this thread's 16 symbols (zero past the chunk), one vector load when aligned
+    uint32_t sw[4] = {0, 0, 0, 0};
+    const uint32_t e0 = 16 * t;
+    const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
+    if (nv == 16 && ((ch.start + e0) & 15u) == 0) {
+        const uint4 v = *(const uint4 *)(L + ch.start + e0);
+        sw[0] = v.x;
+        sw[1] = v.y;
+        sw[2] = v.z;
+        sw[3] = v.w;
+    } else {
+        for (uint32_t k = 0; k < nv; ++k) sw[k >> 2] |= (uint32_t)L[ch.start + e0 + k] << (8 * (k & 3));
+    }
     __syncthreads();
-    for (uint32_t i = t; i < ch.len; i += 256) atomicMax(&lastpos[L[ch.start + i]], (int)i);
+    for (uint32_t k = 0; k < nv; ++k) atomicMax(&lastpos[(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
     __syncthreads();
     const int lp = lastpos[t];
     if (lp >= 0) atomicOr(&bset[lp >> 5], 1u << (lp & 31));
@@ -56,18 +71,12 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
     // thread t owns positions [16t, 16t+16); ranks count set bits at higher positions
     const uint32_t v = (bset[t >> 1] >> (16 * (t & 1))) & 0xffffu;
     const uint32_t cnt = __builtin_popcount(v);
-    const uint32_t rt = 255 - t;  // reversed order -> exclusive sum = bits at higher positions
-    uint32_t off = 0;
-    {
-        // exclusive prefix over reversed thread order
-        uint32_t total;
-        const uint32_t ex_rev = block_excl_sum<256>(cnt, s_tmp, &total);  // sum over threads < t
-        off = total - ex_rev - cnt;                                         // sum over threads > t
-        (void)rt;
-    }
+    uint32_t total;
+    const uint32_t ex = block_excl_sum<256>(cnt, s_tmp, &total);  // set bits in threads < t
+    uint32_t off = total - ex - cnt;                               // set bits in threads > t
     uint8_t *Rc = R + (size_t)blockIdx.x * 256;
     for (int b = 15; b >= 0; --b)
-        if (v & (1u << b)) Rc[off++] = L[ch.start + 16 * t + b];
+        if (v & (1u << b)) Rc[off++] = (uint8_t)(sw[b >> 2] >> (8 * (b & 3)));
     if (t == 0) dcount[blockIdx.x] = (uint32_t)d;
 }
 
@@ -150,22 +159,67 @@ __device__ __forceinline__ void window_reset(uint32_t *bits, uint32_t *cnt, uint
     now = 256;
 }
 
-// One MTF step for symbol c on this lane's state (slot `now`); returns the MTF index.
-__device__ __forceinline__ uint32_t mtf_step(uint32_t c, uint16_t *tm, uint32_t *bits, uint32_t *cnt, uint32_t l,
-                                             uint32_t &S, uint32_t now)
+
+// MTF of G consecutive symbols of one lane with ONE round of state reads (batched step).
+// All reads see the state before the group; in registers, for symbol j:
+//   first occurrence in the group: idx = marks above its stamp + #{i < j first in the group
+//                                  whose stamp is below it} (those moved above it);
+//   repeat of position p:          idx = #distinct symbols in (p, j) = popcount of the
+//                                  "latest occurrence" set above p.
+// Then the state update: each first occurrence clears its old mark, each last occurrence
+// takes slot now0 + j (one OR per group: the G slots share a word).
+template <int G>
+__device__ __forceinline__ uint32_t mtf_group(const uint32_t (&c)[G], uint32_t vmask, uint16_t *tm, uint32_t *bits,
+                                              uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t now0,
+                                              uint32_t (&idx)[G])
 {
-    const uint32_t t = tm[c * kLanes + l];
-    const uint32_t idx = marks_above(t, S, bits, cnt, l);
-    const uint32_t ws = t >> 5, wq = ws >> 2;
-    tm[c * kLanes + l] = (uint16_t)now;
-    atomicXor(&bits[ws * kLanes + l], 1u << (t & 31u));
-    atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
-    S -= 1u << (8 * wq);
-    const uint32_t wn = now >> 5;
-    atomicOr(&bits[wn * kLanes + l], 1u << (now & 31u));
-    atomicAdd(&cnt[(wn >> 2) * kLanes + l], 1u << (8 * (wn & 3u)));
-    S += 1u << (8 * (wn >> 2));
-    return idx;
+    uint32_t t[G], base[G], prev[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) t[j] = tm[c[j] * kLanes + l];
+#pragma unroll
+    for (int j = 0; j < G; ++j) base[j] = marks_above(t[j], S, bits, cnt, l);
+    uint32_t first = 0, lastm = vmask;
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        prev[j] = G;
+#pragma unroll
+        for (int i = 0; i < j; ++i)
+            if (((vmask >> i) & 1u) && c[i] == c[j]) prev[j] = i;
+        if (((vmask >> j) & 1u) && prev[j] == G) first |= 1u << j;
+        if (((vmask >> j) & 1u) && prev[j] < G) lastm &= ~(1u << prev[j]);
+    }
+    uint32_t M = 0;  // latest-occurrence positions among the group's symbols so far
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        uint32_t r;
+        if ((first >> j) & 1u) {
+            r = base[j];
+#pragma unroll
+            for (int i = 0; i < j; ++i) r += ((first >> i) & 1u) && t[i] < t[j];
+        } else {
+            r = __builtin_popcount(M >> (prev[j] + 1));
+        }
+        idx[j] = r;
+        if ((vmask >> j) & 1u) M = (M & ~(prev[j] < G ? 1u << prev[j] : 0u)) | (1u << j);
+    }
+    // state update: clear the old marks of first occurrences, set the last occurrences' slots
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+        if ((first >> j) & 1u) {
+            const uint32_t ws = t[j] >> 5, wq = ws >> 2;
+            atomicXor(&bits[ws * kLanes + l], 1u << (t[j] & 31u));
+            atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
+            S -= 1u << (8 * wq);
+        }
+    }
+    const uint32_t wn = now0 >> 5, np = __builtin_popcount(lastm);
+    atomicOr(&bits[wn * kLanes + l], lastm << (now0 & 31u));
+    atomicAdd(&cnt[(wn >> 2) * kLanes + l], np << (8 * (wn & 3u)));
+    S += np << (8 * (wn >> 2));
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+        if ((lastm >> j) & 1u) tm[c[j] * kLanes + l] = (uint16_t)(now0 + j);
+    return 0;
 }
 
 // grid = ceil(chunks / 256); one lane per chunk. Chunks start 16-byte aligned except a block's
@@ -195,37 +249,61 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
     window_reset(bits, cnt, l, S, now);
     const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
     const uint32_t ngroups = live ? (((end + 15u) & ~15u) - base) >> 4 : 0u;
+    // the input of group g (16 symbols, zero outside the chunk); fetched two groups ahead
+    auto load_group = [&](uint32_t gi) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        const uint32_t a = base + 16 * gi;
+        if (gi < ngroups) {
+            if (a >= ch.start && a + 16 <= end) {
+                v = *(const uint4 *)(L + a);
+            } else {
+                uint32_t *vw = &v.x;
+                for (uint32_t k = 0; k < 16; ++k)
+                    if (a + k >= ch.start && a + k < end) vw[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
+            }
+        }
+        return v;
+    };
+    uint4 pf0 = load_group(0), pf1 = load_group(1);
     for (uint32_t grp = 0; __builtin_amdgcn_ballot_w64(grp < ngroups) != 0; ++grp) {
         const uint32_t a = base + 16 * grp;
         const bool full = grp < ngroups && a >= ch.start && a + 16 <= end;
-        uint4 in4 = make_uint4(0, 0, 0, 0);
-        if (full) {
-            in4 = *(const uint4 *)(L + a);
-        } else if (grp < ngroups) {
-            uint32_t *iw = &in4.x;
-            for (uint32_t k = 0; k < 16; ++k)
-                if (a + k >= ch.start && a + k < end) iw[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
-        }
-        uint4 o4;
+        const uint4 in4 = pf0;
+        pf0 = pf1;
+        pf1 = load_group(grp + 2);
+        uint4 o4 = make_uint4(0, 0, 0, 0);
         uint32_t *o = &o4.x;
         const uint32_t *iw = &in4.x;
+        uint32_t vm = 0;  // symbols of this group that belong to the lane's chunk
+        if (grp < ngroups)
+            for (uint32_t k = 0; k < 16; ++k) vm |= (uint32_t)(a + k >= ch.start && a + k < end) << k;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            uint32_t ow = 0;
+        for (int h = 0; h < 16 / kMtfGroup; ++h) {
+            uint32_t cs[kMtfGroup], ix[kMtfGroup];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t pos = a + 4 * w + k;
-                if (grp < ngroups && pos >= ch.start && pos < end)
-                    ow |= mtf_step((iw[w] >> (8 * k)) & 255u, tm, bits, cnt, l, S, now) << (8 * k);
-                if (++now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
-                    for (uint32_t s = 0; s < 256; ++s) {
-                        const uint32_t ts = tm[s * kLanes + l];
-                        tm[s * kLanes + l] = (uint16_t)(255 - marks_above(ts, S, bits, cnt, l));
-                    }
-                    window_reset(bits, cnt, l, S, now);
-                }
+            for (int j = 0; j < kMtfGroup; ++j) {
+                const int k = h * kMtfGroup + j;
+                cs[j] = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
             }
-            o[w] = ow;
+            mtf_group<kMtfGroup>(cs, (vm >> (h * kMtfGroup)) & ((1u << kMtfGroup) - 1), tm, bits, cnt, l, S, now, ix);
+#pragma unroll
+            for (int j = 0; j < kMtfGroup; ++j) {
+                const int k = h * kMtfGroup + j;
+                o[k >> 2] |= (ix[j] & 255u) << (8 * (k & 3));
+            }
+            now += kMtfGroup;
+            if (now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
+                for (uint32_t s0 = 0; s0 < 256; s0 += 16) {  // 16 independent reads in flight
+                    uint32_t ts[16];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) ts[k] = tm[(s0 + k) * kLanes + l];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) ts[k] = 255 - marks_above(ts[k], S, bits, cnt, l);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) tm[(s0 + k) * kLanes + l] = (uint16_t)ts[k];
+                }
+                window_reset(bits, cnt, l, S, now);
+            }
         }
         if (full) {
             *(uint4 *)(out + a) = o4;
