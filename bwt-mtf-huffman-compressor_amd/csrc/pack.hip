@@ -84,23 +84,26 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
 {
     __shared__ uint64_t s_code[256];
     __shared__ uint8_t s_len[256];
-    __shared__ uint64_t s_tmp[8];
+    __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_img[kPackChunk * 64 / 32 + 2];
     if (status && (*status & kStatusCapacity)) return;
     const PChunk ch = chunks[blockIdx.x];
+    // this thread's 16 symbols first, so their latency overlaps the code-table loads
+    uint8_t sym[kPackIPT];
+    const uint32_t i0 = threadIdx.x * kPackIPT;
+    const bool vec = i0 + kPackIPT <= ch.len && ((ch.start + i0) & 15u) == 0;
+    uint4 v4 = make_uint4(0, 0, 0, 0);
+    if (vec) v4 = *(const uint4 *)(mtf + ch.start + i0);
     const DevTable *t = &tabs[ch.block];
     s_code[threadIdx.x] = t->code[threadIdx.x];
     s_len[threadIdx.x] = t->len[threadIdx.x];
-    __syncthreads();
     const uint64_t P = pay_offs[ch.block] * 8;   // the block's first payload bit
     const uint64_t G = P + cboff[blockIdx.x];    // this chunk's first bit
     const uint64_t W0 = G >> 5;
     const uint32_t sh0 = (uint32_t)(G & 31u);
-    uint8_t sym[kPackIPT];
-    uint64_t mybits = 0;
-    const uint32_t i0 = threadIdx.x * kPackIPT;
-    if (i0 + kPackIPT <= ch.len && ((ch.start + i0) & 15u) == 0) {
-        const uint4 v4 = *(const uint4 *)(mtf + ch.start + i0);
+    __syncthreads();
+    uint32_t mybits = 0;  // a chunk holds at most 4096 * 64 bits
+    if (vec) {
         const uint32_t *vw = &v4.x;
 #pragma unroll
         for (uint32_t k = 0; k < kPackIPT; ++k) {
@@ -114,8 +117,9 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
             mybits += i < ch.len ? s_len[sym[k]] : 0u;
         }
     }
-    uint64_t total;
-    uint64_t tb = block_excl_sum64<256>(mybits, s_tmp, &total) + sh0;
+    uint32_t total32;
+    uint64_t tb = block_excl_sum<256>(mybits, s_tmp, &total32) + sh0;
+    const uint64_t total = total32;
     // the block's last chunk also owns the zero pad bits up to the payload's last byte
     // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
     const bool last = blockIdx.x + 1 == cfirst[ch.block + 1];
