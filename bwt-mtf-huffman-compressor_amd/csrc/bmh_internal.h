@@ -7,6 +7,8 @@
 #include <cstdint>
 #include <cstring>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -73,6 +75,10 @@ struct Ctx {
         size_t off, bytes;
     };
     std::vector<Deferred> deferred;
+
+    // sub-pipelines (own stream + workspaces) a batch is split across (capi.cpp)
+    std::vector<Ctx *> subs;
+    int nstreams = 0;  // 0: BMH_STREAMS or the default
 
     void *get(Slot s, size_t bytes);
     void *host_pinned(size_t bytes);
@@ -152,9 +158,19 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                uint32_t *h_first32);
 void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
                 const uint64_t *pay_offs);
+// Record offsets of consecutive sub-batches encoded concurrently on several streams: sub-batch
+// s starts where s - 1 ends (a device value), so s waits for s - 1's offset scan.
+struct OffsetChain {
+    std::mutex m;
+    std::condition_variable cv;
+    int recorded = -1;  // highest sub-batch whose offset scan has been enqueued
+    bool failed = false;
+    std::vector<hipEvent_t> ev;
+    std::vector<const uint64_t *> d_end;  // device: end offset of each sub-batch's records
+};
 void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint32_t *d_freq, const uint32_t *d_first,
                     const uint32_t *d_prim, DevTable *d_tabs, uint64_t *d_roffs, uint64_t *d_pay_offs,
-                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status);
+                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status, OffsetChain *chain, int sub);
 void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
                     uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist);
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);

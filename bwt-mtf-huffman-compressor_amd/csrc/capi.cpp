@@ -164,8 +164,8 @@ Batch make_batch(const uint64_t *offs, uint32_t nblocks)
 uint64_t record_bound(uint64_t n) { return kRecordHeader + 320 + n + 16; }
 
 // Device batch encode -> records at d_out; fills rec_offs (nblocks + 1).
-void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
-                   uint64_t *rec_offs)
+static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
+                              uint64_t *rec_offs, OffsetChain *chain, int sub)
 {
     // BWT -> MTF (+ histograms) -> code books, record offsets and headers -> bit pack, all
     // on the context stream; the host waits on the BWT's list counters, and once at the end
@@ -192,7 +192,8 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     uint64_t *d_boffs = (uint64_t *)(d_misc + 64);
     BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
     c->h2d(d_boffs, bt.offs.data(), (nb + 1) * 8);
-    codebook_batch(c, bt, d_boffs, d_freq, d_first, d_prim, d_tabs, d_roffs, d_pay_offs, d_out, out_cap, d_status);
+    codebook_batch(c, bt, d_boffs, d_freq, d_first, d_prim, d_tabs, d_roffs, d_pay_offs, d_out, out_cap, d_status, chain,
+                   sub);
     const uint16_t *d_chist = (const uint16_t *)c->get(WS_PACK_HIST, 64);  // written by mtf_batch
     pack_batch_dev(c, d_mtf, bt, d_tabs, d_pay_offs, d_out, d_status, d_chist);
     uint32_t st = 0;
@@ -203,6 +204,107 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     if (st & kStatusEmpty) fail(BMH_EINVAL, "huffman: empty histogram (the reference segfaults on empty input)");
     if (st & kStatusCodeLen) fail(BMH_ERANGE, "huffman: code longer than 64 bits");
     if (st & kStatusPrimary) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
+}
+
+static Ctx *sub_ctx(Ctx *c, size_t i)
+{
+    while (c->subs.size() <= i) {
+        Ctx *x = new bmh_ctx();
+        x->device = c->device;
+        if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
+            delete x;
+            fail(BMH_EHIP, "stream creation failed");
+        }
+        c->subs.push_back(x);
+    }
+    Ctx *x = c->subs[i];
+    x->timing = c->timing;
+    return x;
+}
+
+static int stream_count(Ctx *c)
+{
+    if (c->nstreams > 0) return c->nstreams;
+    const char *e = getenv("BMH_STREAMS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? std::min(v, 16) : 2;
+}
+
+// The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
+// stream by its own host thread, so that one run's bandwidth-bound kernels overlap another's
+// LDS-bound ones. Records land back to back in block order: each run's offset scan starts
+// from the previous run's end (OffsetChain).
+void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
+                   uint64_t *rec_offs)
+{
+    const uint32_t nb = bt.nblocks;
+    const int S = (int)std::min<uint32_t>((uint32_t)stream_count(c), nb / 2);
+    if (S <= 1) {
+        encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
+        return;
+    }
+    std::vector<uint32_t> cut(S + 1, nb);
+    cut[0] = 0;
+    for (int s = 1; s < S; ++s) {
+        const uint64_t target = bt.total * s / S;
+        uint32_t b = cut[s - 1] + 1;
+        while (b < nb - (uint32_t)(S - s) && bt.offs[b] < target) ++b;
+        cut[s] = b;
+    }
+    OffsetChain chain;
+    chain.ev.resize(S);
+    chain.d_end.resize(S, nullptr);
+    std::vector<Ctx *> cs(S);
+    for (int s = 0; s < S; ++s) {
+        cs[s] = sub_ctx(c, s);
+        BMH_HIP(hipEventCreateWithFlags(&chain.ev[s], hipEventDisableTiming));
+    }
+    std::vector<std::vector<uint64_t>> ro(S);
+    std::vector<bmh_status> st(S, BMH_OK);
+    std::vector<std::string> err(S);
+    auto run = [&](int s) {
+        try {
+            BMH_HIP(hipSetDevice(c->device));
+            Batch sb;
+            sb.nblocks = cut[s + 1] - cut[s];
+            sb.offs.resize(sb.nblocks + 1);
+            for (uint32_t i = 0; i <= sb.nblocks; ++i) sb.offs[i] = bt.offs[cut[s] + i] - bt.offs[cut[s]];
+            sb.total = sb.offs[sb.nblocks];
+            for (uint32_t i = 0; i < sb.nblocks; ++i)
+                sb.max_n = std::max<uint32_t>(sb.max_n, (uint32_t)(sb.offs[i + 1] - sb.offs[i]));
+            ro[s].resize(sb.nblocks + 1);
+            encode_blocks_one(cs[s], d_in + bt.offs[cut[s]], sb, d_out, out_cap, ro[s].data(), &chain, s);
+        } catch (const Error &e) {
+            st[s] = e.status;
+            err[s] = e.what();
+        } catch (const std::exception &e) {
+            st[s] = BMH_EHIP;
+            err[s] = e.what();
+        }
+        if (st[s] != BMH_OK) {
+            std::lock_guard<std::mutex> lk(chain.m);
+            chain.failed = true;
+            chain.cv.notify_all();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int s = 1; s < S; ++s) th.emplace_back(run, s);
+    run(0);
+    for (auto &t : th) t.join();
+    for (int s = 0; s < S; ++s) (void)hipEventDestroy(chain.ev[s]);
+    if (c->timing)  // fold the sub-pipelines' kernel times into the parent's statistics
+        for (int s = 0; s < S; ++s) {
+            for (auto &kv : cs[s]->stats) {
+                c->stats[kv.first].launches += kv.second.launches;
+                c->stats[kv.first].ms += kv.second.ms;
+            }
+            cs[s]->stats.clear();
+        }
+    for (int s = 0; s < S; ++s)
+        if (st[s] != BMH_OK) fail(st[s], err[s]);
+    for (int s = 0; s < S; ++s)
+        for (uint32_t i = 0; i < cut[s + 1] - cut[s]; ++i) rec_offs[cut[s] + i] = ro[s][i];
+    rec_offs[nb] = ro[S - 1][cut[S] - cut[S - 1]];
 }
 
 static uint64_t max_batch_bytes()
@@ -364,6 +466,9 @@ bmh_status bmh_ctx_create(int device, bmh_ctx **out)
 void bmh_ctx_destroy(bmh_ctx *c)
 {
     if (!c) return;
+    for (auto *x : c->subs) bmh_ctx_destroy(static_cast<bmh_ctx *>(x));
+    c->subs.clear();
+    if (c->arena) (void)hipHostFree(c->arena);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (int s = 0; s < WS_COUNT_; ++s)

@@ -220,10 +220,11 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
 // One workgroup: record offsets = exclusive scan of (header + payload) sizes.
 __global__ __launch_bounds__(1024) void k_rec_offs(uint32_t nb, const uint32_t *__restrict__ hdr_len,
                                                    const uint64_t *__restrict__ pay_bytes, uint64_t *__restrict__ roffs,
-                                                   uint64_t *__restrict__ pay_offs, uint64_t out_cap, uint32_t *status)
+                                                   uint64_t *__restrict__ pay_offs, uint64_t out_cap, uint32_t *status,
+                                                   const uint64_t *base)
 {
     __shared__ uint64_t s_tmp[17];
-    uint64_t carry = 0;
+    uint64_t carry = base ? *base : 0ull;  // sub-batches chain on the previous one's end
     for (uint32_t base = 0; base < nb; base += 1024) {
         const uint32_t b = base + threadIdx.x;
         const uint64_t v = b < nb ? hdr_len[b] + pay_bytes[b] : 0ull;
@@ -256,7 +257,7 @@ __global__ __launch_bounds__(64) void k_rec_headers(const uint8_t *__restrict__ 
 
 void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint32_t *d_freq, const uint32_t *d_first,
                     const uint32_t *d_prim, DevTable *d_tabs, uint64_t *d_roffs, uint64_t *d_pay_offs,
-                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status)
+                    uint8_t *d_out, uint64_t out_cap, uint32_t *d_status, OffsetChain *chain, int sub)
 {
     const uint32_t nb = bt.nblocks;
     uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, (size_t)nb * kHdrStride + (size_t)nb * 12 + 64);
@@ -264,7 +265,24 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
     uint32_t *d_hlen = (uint32_t *)(d_payb + nb);
     BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
                d_status);
-    BMH_LAUNCH(c, "rec_offs", k_rec_offs, 1, 1024, 0, nb, d_hlen, d_payb, d_roffs, d_pay_offs, out_cap, d_status);
+    const uint64_t *d_base = nullptr;
+    if (chain && sub > 0) {
+        std::unique_lock<std::mutex> lk(chain->m);
+        chain->cv.wait(lk, [&] { return chain->recorded >= sub - 1 || chain->failed; });
+        if (chain->failed) fail(BMH_EHIP, "encode: a concurrent sub-batch failed");
+        BMH_HIP(hipStreamWaitEvent(c->stream, chain->ev[sub - 1], 0));
+        d_base = chain->d_end[sub - 1];
+    }
+    BMH_LAUNCH(c, "rec_offs", k_rec_offs, 1, 1024, 0, nb, d_hlen, d_payb, d_roffs, d_pay_offs, out_cap, d_status, d_base);
+    if (chain) {
+        BMH_HIP(hipEventRecord(chain->ev[sub], c->stream));
+        {
+            std::lock_guard<std::mutex> lk(chain->m);
+            chain->d_end[sub] = d_roffs + nb;
+            chain->recorded = sub;
+        }
+        chain->cv.notify_all();
+    }
     BMH_LAUNCH(c, "rec_headers", k_rec_headers, nb, 64, 0, d_hdr, d_hlen, d_roffs, d_out, d_status);
 }
 
