@@ -415,7 +415,8 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         if (m > 1) {
             const uint32_t r = rv[k];
             eqt = 0;
-            for (uint32_t f = s0; f < s1; ++f) {
+#pragma nounroll
+            for (uint32_t f = s0; f < s1; ++f) {  // sub-buckets are short (~1-4 on random data)
                 const uint32_t rf = s_rest[f];
                 lt += rf < r;
                 const bool eq = rf == r;
