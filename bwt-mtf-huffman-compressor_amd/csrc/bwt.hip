@@ -245,7 +245,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     __shared__ uint16_t s_ent[kG1Chunk];  // chunk-relative position
     // byte j <-> block position start - 4 + j (cyclic), j < len + 12
     __shared__ uint32_t s_txt[(kG1Chunk + 12) / 4 + 1];
-    __shared__ uint32_t s_cnt[kG1Bins], s_ls[kG1Bins], s_off[kG1Bins], s_blen[kG1Bins];
+    __shared__ uint32_t s_cnt[kG1Bins], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
     __shared__ uint32_t s_tmp[17];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     {
         static_assert(kG1Bins == 1024, "one digit per thread");
         const uint32_t ex = block_excl_sum<1024>(s_cnt[t], s_tmp, nullptr);
-        s_ls[t] = ex;
+        s_off[t] -= ex;  // slot of local element i with digit d = s_off[d] + i
         s_cnt[t] = ex;
     }
     __syncthreads();
@@ -316,7 +316,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint64_t b8 = (d2 >> al) & 255u;                                       // byte j0 + 8
         const uint64_t key = __builtin_bswap64((v64 >> 16) | (b8 << 48)) | (v64 & 255u);
         const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
-        const uint32_t slot = s_off[d] + (i - s_ls[d]);
+        const uint32_t slot = s_off[d] + i;
         const uint32_t blen = s_blen[d];
         if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
             const uint32_t P = rec_pbits(n), R = rec_rbits(P);

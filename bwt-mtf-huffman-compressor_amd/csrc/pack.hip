@@ -140,24 +140,30 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
         uint32_t w = (uint32_t)(tb >> 5), nacc = (uint32_t)(tb & 31u);
         const bool head_shared = nacc != 0;
         uint64_t acc = 0;
+        const uint32_t w_head = (uint32_t)(tb >> 5);
+        auto push = [&](uint32_t v, uint32_t l) {  // l <= 32 bits, MSB-first
+            if (l) {
+                acc |= ((uint64_t)v << (64 - l)) >> nacc;
+                nacc += l;
+            }
+            if (nacc >= 32) {
+                const uint32_t word = (uint32_t)(acc >> 32);
+                if (w == w_head && head_shared) atomicOr(&s_img[w], word);
+                else s_img[w] = word;
+                ++w;
+                acc <<= 32;
+                nacc -= 32;
+            }
+        };
         for (uint32_t k = 0; k < kPackIPT; ++k) {
             if (i0 + k >= ch.len) break;
-            uint32_t l = s_len[sym[k]];
+            const uint32_t l = s_len[sym[k]];
             const uint64_t code = s_code[sym[k]];
-            while (l > 0) {
-                const uint32_t take = min(l, 32u);
-                const uint64_t piece = (code >> (l - take)) & ((1ull << take) - 1);
-                acc |= piece << (64 - nacc - take);
-                nacc += take;
-                l -= take;
-                if (nacc >= 32) {
-                    const uint32_t word = (uint32_t)(acc >> 32);
-                    if (w == (uint32_t)(tb >> 5) && head_shared) atomicOr(&s_img[w], word);
-                    else s_img[w] = word;
-                    ++w;
-                    acc <<= 32;
-                    nacc -= 32;
-                }
+            if (l > 32) {  // codes longer than 32 bits (never on 8-bit alphabets in practice)
+                push((uint32_t)(code >> 32), l - 32);
+                push((uint32_t)code, 32);
+            } else {
+                push((uint32_t)code, l);
             }
         }
         if (nacc) atomicOr(&s_img[w], (uint32_t)(acc >> 32));
