@@ -77,6 +77,8 @@ _SIGS = {
     "bmh_compress_bound": (U64, [U64, U64]),
     "bmh_decompress_host": (C.c_int, [P, U64, P, U64, PU64]),
     "bmh_record_to_mtf": (C.c_int, [P, U64, P, U64, PU64]),
+    "bmh_decode_blocks_dev": (C.c_int, [P, P, PU64, U32, P, U64, PU64]),
+    "bmh_decompress_dev": (C.c_int, [P, P, U64, P, U64, PU64]),
     "bmh_is_container": (C.c_int, [P, U64]),
     "bmh_container_info": (C.c_int, [P, U64, PU64, PU64]),
     "bmh_container_record": (C.c_int, [P, U64, U64, C.POINTER(P), PU64]),
@@ -227,6 +229,23 @@ class Context:
         _check(lib().bmh_encode_blocks_dev(self.h, _dp(d_in), _u64p(offs), len(offs) - 1, _dp(d_out), out_cap,
                                            _u64p(ro)), "encode_blocks")
         return ro
+
+    def decode_blocks_dev(self, d_rec, rec_offs: np.ndarray, d_out, out_cap: int) -> np.ndarray:
+        """GPU decode of records in device memory; returns the output offsets (nblocks+1)."""
+        rec_offs = np.ascontiguousarray(rec_offs, dtype=np.uint64)
+        oo = np.zeros(len(rec_offs), dtype=np.uint64)
+        _check(lib().bmh_decode_blocks_dev(self.h, _dp(d_rec), _u64p(rec_offs), len(rec_offs) - 1, _dp(d_out),
+                                           out_cap, _u64p(oo)), "decode_blocks")
+        return oo
+
+    def decompress_bytes(self, data) -> bytes:
+        """decompress() (main.cpp:327-345) of a record or container, decoded on this GPU."""
+        a = as_u8(data)
+        n = C.c_uint64()
+        _check(lib().bmh_decompress_dev(self.h, _ptr(a), a.size, None, 0, C.byref(n)), "decompress_dev(size)")
+        out = np.empty(max(n.value, 1), dtype=np.uint8)
+        _check(lib().bmh_decompress_dev(self.h, _ptr(a), a.size, _ptr(out), n.value, C.byref(n)), "decompress_dev")
+        return out[: n.value].tobytes()
 
     def synth_splitmix64(self, d_out, nbytes: int, seed: int = 0, offset: int = 0) -> None:
         _check(lib().bmh_synth_splitmix64_dev(self.h, _dp(d_out), nbytes, seed, offset), "synth")

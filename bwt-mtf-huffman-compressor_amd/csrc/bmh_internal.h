@@ -180,6 +180,20 @@ void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, ui
 void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out);
 uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);
 
+// Device Huffman decode table of one record (built on the host by build_dec_table).
+constexpr uint32_t kDecLutBits = 12;
+struct DecTable {
+    uint32_t lut[1u << kDecLutBits];  // next 12 bits -> sym << 8 | code length, or node << 16 (longer code)
+    uint16_t child[512][2];           // internal nodes: children (node ids); leaves: 0xffff
+    uint8_t sym[512];                 // leaf symbols
+    uint32_t single;                  // the root is a leaf: every symbol is sym[0], 0-bit codes
+    uint32_t pad[3];
+};
+// Parses the preorder tree bytes of a record (bytes_to_tree_dfs, main.cpp:198-219).
+void build_dec_table(const uint8_t *tree, uint64_t tree_len, DecTable *out);
+void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint32_t nblocks, uint8_t *d_out,
+                   uint64_t out_cap, uint64_t *out_offs);
+
 // Records / container / decode (record.cpp)
 constexpr uint64_t kRecordHeader = 24;
 void put_u64(uint8_t *p, uint64_t v);
@@ -188,6 +202,11 @@ extern const uint8_t kContainerMagic[8];
 uint64_t record_n(const uint8_t *rec, uint64_t len);
 void record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out);
 void decode_record(const uint8_t *rec, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
+struct ContainerView {
+    uint64_t block_size, nblocks, total;
+    std::vector<uint64_t> rec_off, rec_len;
+};
+ContainerView parse_container(const uint8_t *in, uint64_t len);
 bool is_container(const uint8_t *in, uint64_t len);
 void decompress(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
 

@@ -667,6 +667,67 @@ bmh_status bmh_decompress_host(const uint8_t *in, uint64_t len, uint8_t *out, ui
     API_END
 }
 
+bmh_status bmh_decode_blocks_dev(bmh_ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint32_t nblocks,
+                                 uint8_t *d_out, uint64_t out_cap, uint64_t *h_out_offs)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_rec || !rec_offs || !d_out || !h_out_offs || nblocks == 0) fail(BMH_EINVAL, "null argument");
+    decode_blocks(c, d_rec, rec_offs, nblocks, d_out, out_cap, h_out_offs);
+    API_END
+}
+
+bmh_status bmh_decompress_dev(bmh_ctx *c, const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out)
+{
+    API_BEGIN
+    use_device(c);
+    if (!in || !n_out) fail(BMH_EINVAL, "null argument");
+    // record list (a single record, or the records of a container)
+    std::vector<uint64_t> ro, rl;
+    if (is_container(in, len)) {
+        ContainerView v = parse_container(in, len);
+        ro = v.rec_off;
+        rl = v.rec_len;
+    } else {
+        ro.push_back(0);
+        rl.push_back(len);
+    }
+    uint64_t total = 0;
+    std::vector<uint64_t> ns(ro.size());
+    for (size_t b = 0; b < ro.size(); ++b) {
+        ns[b] = record_n(in + ro[b], rl[b]);
+        total += ns[b];
+    }
+    *n_out = total;
+    if (!out) return BMH_OK;
+    if (total > cap) fail(BMH_ERANGE, "decompress: output capacity too small");
+    // batches of consecutive records: output < 1 GiB (BMH_MAX_BATCH), <= 65535 records
+    const uint64_t cap_batch = max_batch_bytes();
+    uint64_t done = 0;
+    for (size_t i = 0; i < ro.size();) {
+        size_t j = i;
+        uint64_t nout = 0, nin = 0;
+        while (j < ro.size() && j - i < 65535 && (j == i || nout + ns[j] <= cap_batch)) {
+            nout += ns[j];
+            nin += rl[j];
+            ++j;
+        }
+        uint8_t *d_in = (uint8_t *)c->get(WS_IN, nin + 64);
+        uint8_t *d_o = (uint8_t *)c->get(WS_OUT, nout + 64);
+        std::vector<uint64_t> offs(j - i + 1, 0), oo(j - i + 1, 0);
+        for (size_t k = i; k < j; ++k) {
+            BMH_HIP(hipMemcpyAsync(d_in + offs[k - i], in + ro[k], rl[k], hipMemcpyHostToDevice, c->stream));
+            offs[k - i + 1] = offs[k - i] + rl[k];
+        }
+        decode_blocks(c, d_in, offs.data(), (uint32_t)(j - i), d_o, nout, oo.data());
+        BMH_HIP(hipMemcpyAsync(out + done, d_o, nout, hipMemcpyDeviceToHost, c->stream));
+        c->sync();
+        done += nout;
+        i = j;
+    }
+    API_END
+}
+
 bmh_status bmh_record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out)
 {
     API_BEGIN

@@ -146,6 +146,42 @@ void bwt_inverse(const uint8_t *L, uint64_t n, uint64_t primary, uint8_t *out)
 
 }  // namespace
 
+void build_dec_table(const uint8_t *tree, uint64_t tree_len, DecTable *out)
+{
+    BitReader tr{tree, tree_len};
+    DTree t;
+    const int root = t.parse(tr, 0);
+    memset(out, 0, sizeof *out);
+    for (int v = 0; v < t.n; ++v) {
+        out->child[v][0] = t.left[v] < 0 ? 0xffff : (uint16_t)t.left[v];
+        out->child[v][1] = t.right[v] < 0 ? 0xffff : (uint16_t)t.right[v];
+        out->sym[v] = t.sym[v];
+    }
+    if (t.left[root] < 0) {
+        out->single = 1;
+        out->sym[0] = t.sym[root];
+        return;
+    }
+    // fill the LUT by walking the tree: a leaf at depth d <= 12 covers 2^(12-d) entries
+    struct Item {
+        int v;
+        uint32_t code, depth;
+    };
+    std::vector<Item> st{{root, 0, 0}};
+    while (!st.empty()) {
+        const Item it = st.back();
+        st.pop_back();
+        if (t.left[it.v] < 0 || it.depth == kDecLutBits) {
+            const uint32_t span = 1u << (kDecLutBits - it.depth), first = it.code << (kDecLutBits - it.depth);
+            const uint32_t e = t.left[it.v] < 0 ? ((uint32_t)t.sym[it.v] << 8) | it.depth : (uint32_t)it.v << 16;
+            for (uint32_t k = 0; k < span; ++k) out->lut[first + k] = e;
+            continue;
+        }
+        st.push_back({t.right[it.v], (it.code << 1) | 1u, it.depth + 1});
+        st.push_back({t.left[it.v], it.code << 1, it.depth + 1});
+    }
+}
+
 uint64_t record_n(const uint8_t *rec, uint64_t len)
 {
     // header sanity before anyone sizes a buffer from n
@@ -186,11 +222,6 @@ void decode_record(const uint8_t *rec, uint64_t len, uint8_t *out, uint64_t cap,
 }
 
 bool is_container(const uint8_t *in, uint64_t len) { return len >= 8 && memcmp(in, kContainerMagic, 8) == 0; }
-
-struct ContainerView {
-    uint64_t block_size, nblocks, total;
-    std::vector<uint64_t> rec_off, rec_len;
-};
 
 ContainerView parse_container(const uint8_t *in, uint64_t len)
 {

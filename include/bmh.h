@@ -121,6 +121,17 @@ uint64_t bmh_compress_bound(uint64_t n, uint64_t block_size);
 /* Decodes one reference record or one BMH container. *n_out receives the decoded size;
  * if out is NULL only the size is reported. */
 bmh_status bmh_decompress_host(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uint64_t *n_out);
+/* GPU decode (replaces decompress(), main.cpp:327-345 — tree parse :198-219, huffman_reverse
+ * :259-281, inverse MTF :114-130, bwt_reverse :61-75) of a batch of records in device
+ * memory: record b = d_rec[rec_offs[b], rec_offs[b+1]) (rec_offs: host, nblocks+1 entries).
+ * Block b's bytes land at d_out + h_out_offs[b]; h_out_offs (host, nblocks+1) is filled
+ * from the record headers. The batch output must be < 4 GiB. */
+bmh_status bmh_decode_blocks_dev(bmh_ctx *ctx, const uint8_t *d_rec, const uint64_t *rec_offs, uint32_t nblocks,
+                                 uint8_t *d_out, uint64_t out_cap, uint64_t *h_out_offs);
+/* decompress() of a record or BMH container held in host memory, decoded on the GPU (same
+ * contract as bmh_decompress_host). */
+bmh_status bmh_decompress_dev(bmh_ctx *ctx, const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap,
+                              uint64_t *n_out);
 /* Huffman stage inverse only (huffman_reverse, main.cpp:259-281): record -> MTF stream. */
 bmh_status bmh_record_to_mtf(const uint8_t *rec, uint64_t len, uint8_t *mtf, uint64_t cap, uint64_t *n_out);
 

@@ -187,3 +187,37 @@ def test_container_roundtrip(ctx):
     assert bmh.decompress_bytes(out) == data
     one = ctx.encode_blocks([data[: 1 << 20]])[0]
     assert recs[0] == one
+
+
+# ------------------------------------------------------------------------ GPU decode
+def test_gpu_decode_golden_records(ctx):
+    """The reference's own records (Calgary + small known answers) decoded on the GPU."""
+    for name, data, rec in list(golden_calgary()) + list(golden_small()):
+        assert ctx.decompress_bytes(rec) == data, name
+
+
+def test_gpu_decode_edge_roundtrips(ctx):
+    for name in sorted(EDGE):
+        rec = ctx.encode_blocks([EDGE[name]])[0]
+        assert ctx.decompress_bytes(rec) == EDGE[name], name
+
+
+def test_gpu_decode_container_roundtrip(ctx):
+    data = synth.zipf_text(5_000_003).tobytes()
+    out = ctx.compress_bytes(data, block_size=1 << 20)
+    assert ctx.decompress_bytes(out) == data
+
+
+def test_gpu_decode_random_1g_blocks(ctx):
+    # full-size blocks of the bench workload: encode -> GPU decode round trip, 16 x 4 MiB
+    bs, nb = 1 << 22, 16
+    d_in = ctx.alloc(bs * nb)
+    ctx.synth_splitmix64(d_in, bs * nb, 0, 0)
+    offs = np.arange(nb + 1, dtype=np.uint64) * np.uint64(bs)
+    cap = nb * int(bmh.lib().bmh_record_bound(bs))
+    d_rec = ctx.alloc(cap)
+    ro = ctx.encode_blocks_dev(d_in, offs, d_rec, cap)
+    d_dec = ctx.alloc(bs * nb)
+    oo = ctx.decode_blocks_dev(d_rec, ro, d_dec, bs * nb)
+    assert (oo == offs).all()
+    assert d_dec.download().tobytes() == d_in.download().tobytes()
