@@ -122,6 +122,7 @@ def main() -> None:
     ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0, help="blocks in the CPU sample (default: host threads, <=16)")
+    ap.add_argument("--decode-steps", type=int, default=3, help="timed GPU decode steps of the same records (0: skip)")
     a = ap.parse_args()
 
     r = dist.init()
@@ -181,6 +182,23 @@ def main() -> None:
 
     ro = rec_offs[0]
     out_bytes = dist.sum_over_ranks(r, float(ro[-1]))
+    # decode of the same records on the same GPU (GPU decode), timed the same way,
+    # with a full round-trip check of this rank's batch; reported beside the encode line
+    dec = None
+    if a.decode_steps > 0:
+        d_dec = ctx.alloc(total)
+        ro_host = np.ascontiguousarray(ro, dtype=np.uint64)
+
+        def dstep():
+            ctx.decode_blocks_dev(d_out, ro_host, d_dec, total)
+        dstep()
+        ddt = dist.timed_steps(r, dstep, a.decode_steps, 0, sync)
+        ok = d_dec.download().tobytes() == d_in.download().tobytes()
+        ok = dist.sum_over_ranks(r, float(ok)) == world
+        dec = {"value": round(float(total) * world * a.decode_steps / ddt / 1e6, 2), "unit": "MB/s (decoded bytes)",
+               "ms_per_step": round(ddt / a.decode_steps * 1e3, 3), "steps": a.decode_steps,
+               "roundtrip_bit_exact": bool(ok)}
+        d_dec.free()
     in_bytes = float(total) * world
     # parity spot check: this rank's first block vs the reference manifest
     parity = None
@@ -239,6 +257,7 @@ def main() -> None:
             "kernels_ms_per_step": {k: round(v[1] / ksteps, 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
             "host_wall_ms_per_step": {k: round(v[1] / ksteps, 3) for k, v in walls.items()},
             "parity": parity,
+            "decode": dec,
         }
         if world == 1 and not a.no_cpu_baseline:
             ns = a.cpu_sample or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 8)))
