@@ -86,25 +86,101 @@ __device__ __forceinline__ uint32_t dec_sym(const DecTable *__restrict__ t, uint
     return k;
 }
 
+// Decode tables of a workgroup's block staged in LDS (every workgroup of the Huffman passes
+// holds segments of one block: each block's segment list starts on a multiple of 256).
+struct DecLds {
+    uint32_t lut[1u << kDecLutBits];
+    uint32_t child[512];  // lo 16: left, hi 16: right (0xffff: leaf)
+    uint8_t sym[512];
+};
+
+__device__ __forceinline__ void load_dec_lds(DecLds &d, const DecTable *__restrict__ t)
+{
+    for (uint32_t i = threadIdx.x; i < (1u << kDecLutBits); i += 256) d.lut[i] = t->lut[i];
+    for (uint32_t i = threadIdx.x; i < 512; i += 256) {
+        d.child[i] = (uint32_t)t->child[i][0] | ((uint32_t)t->child[i][1] << 16);
+        d.sym[i] = t->sym[i];
+    }
+}
+
+// MSB-first bit window over a payload: win holds the next `valid` (>= 32 after refill) bits.
+struct BitWin {
+    const uint32_t *p;  // next aligned dword to load
+    const uint32_t *pend;  // first dword past the payload
+    uint64_t win;
+    uint32_t valid;
+    __device__ __forceinline__ uint32_t ld(const uint32_t *q) const { return q < pend ? __builtin_bswap32(*q) : 0u; }
+    __device__ __forceinline__ void init(const uint8_t *pay, uint64_t pay_bits, uint64_t pos)
+    {
+        const uint64_t abit = (uint64_t)(uintptr_t)pay * 8 + pos;  // absolute bit address
+        const uint32_t *q = (const uint32_t *)(uintptr_t)((abit >> 5) << 2);
+        pend = (const uint32_t *)(((uintptr_t)pay + (pay_bits >> 3) + 3) & ~(uintptr_t)3);
+        const uint32_t o = (uint32_t)(abit & 31u);
+        win = (((uint64_t)ld(q) << 32) | ld(q + 1)) << o;
+        valid = 64 - o;
+        p = q + 2;
+    }
+    __device__ __forceinline__ void refill()
+    {
+        if (valid < 32) {
+            win |= (uint64_t)ld(p) << (32 - valid);
+            valid += 32;
+            ++p;
+        }
+    }
+    __device__ __forceinline__ void consume(uint32_t n)
+    {
+        win = n < 64 ? win << n : 0ull;
+        valid -= n;
+    }
+};
+
+// one symbol from the window (codes up to 32 + 12 bits wide are decoded from the window;
+// the window always holds >= 32 bits here)
+__device__ __forceinline__ uint32_t dec_sym_lds(const DecLds &d, uint64_t w, uint32_t &sym)
+{
+    const uint32_t e = d.lut[w >> (64 - kDecLutBits)];
+    if (e & 255u) {
+        sym = (e >> 8) & 255u;
+        return e & 255u;
+    }
+    uint32_t v = e >> 16, k = kDecLutBits;
+    while (true) {
+        const uint32_t ch = d.child[v];
+        v = ((w >> (63 - k)) & 1u) ? ch >> 16 : ch & 0xffffu;
+        ++k;
+        if ((d.child[v] & 0xffffu) == 0xffffu || k >= 64) break;
+    }
+    sym = d.sym[v];
+    return k;
+}
+
 __global__ __launch_bounds__(256) void k_hd_pass1(const DBlock *__restrict__ blks, const DecTable *__restrict__ tabs,
                                                   const uint32_t *__restrict__ seg_block, uint32_t nseg_total,
                                                   uint64_t *__restrict__ seg_end, uint32_t *__restrict__ seg_cnt,
                                                   uint16_t *__restrict__ bnd)
 {
+    __shared__ DecLds d;
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= nseg_total) return;
-    const uint32_t b = seg_block[g];
-    const DBlock B = blks[b];
-    const DecTable *t = &tabs[b];
+    const uint32_t bw = seg_block[blockIdx.x * 256];  // the workgroup's block
+    load_dec_lds(d, &tabs[bw]);
+    __syncthreads();
+    if (g >= nseg_total || seg_block[g] == kNil) return;
+    const DBlock B = blks[bw];
     const uint64_t s0 = (uint64_t)(g - B.seg0) * kSegBits;
     const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
     uint64_t pos = s0;
     uint32_t cnt = 0;
     uint16_t *bb = bnd + (size_t)g * kSyncBnd;
+    BitWin r;
+    r.init(B.pay, B.pay_bits, pos);
     while (pos < stop) {
         if (cnt < kSyncBnd) bb[cnt] = (uint16_t)(pos - s0);
+        r.refill();
         uint32_t sym;
-        pos += dec_sym(t, bits64(B.pay, B.pay_bits, pos), sym);
+        const uint32_t len = dec_sym_lds(d, r.win, sym);
+        r.consume(len);
+        pos += len;
         ++cnt;
     }
     for (uint32_t k = cnt; k < kSyncBnd; ++k) bb[k] = 0xffff;
@@ -121,7 +197,7 @@ __global__ __launch_bounds__(256) void k_hd_fix(const DBlock *__restrict__ blks,
                                                 const uint16_t *__restrict__ bnd, uint32_t *changed)
 {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= nseg_total) return;
+    if (g >= nseg_total || seg_block[g] == kNil) return;
     const uint32_t b = seg_block[g];
     const DBlock B = blks[b];
     const uint64_t s0 = (uint64_t)(g - B.seg0) * kSegBits;
@@ -182,21 +258,42 @@ __global__ __launch_bounds__(256) void k_hd_pass3(const DBlock *__restrict__ blk
                                                   const uint32_t *__restrict__ seg_first, uint8_t *__restrict__ mtf,
                                                   uint32_t *status)
 {
+    __shared__ DecLds d;
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= nseg_total) return;
-    const uint32_t b = seg_block[g];
-    const DBlock B = blks[b];
-    const DecTable *t = &tabs[b];
+    const uint32_t bw = seg_block[blockIdx.x * 256];
+    load_dec_lds(d, &tabs[bw]);
+    __syncthreads();
+    if (g >= nseg_total || seg_block[g] == kNil) return;
+    const DBlock B = blks[bw];
     const uint64_t s0 = (uint64_t)(g - B.seg0) * kSegBits;
     const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
     uint64_t pos = seg_start[g];
     uint32_t i = seg_first[g];
     uint8_t *o = mtf + B.out_off;
+    BitWin r;
+    r.init(B.pay, B.pay_bits, pos);
+    // symbols are written four at a time once the output address is word-aligned
+    uint32_t acc = 0, na = 0;
     while (pos < stop && i < B.n) {
+        r.refill();
         uint32_t sym;
-        pos += dec_sym(t, bits64(B.pay, B.pay_bits, pos), sym);
-        o[i++] = (uint8_t)sym;
+        const uint32_t len = dec_sym_lds(d, r.win, sym);
+        r.consume(len);
+        pos += len;
+        const uint64_t a = B.out_off + i;
+        if (na == 0 && (a & 3u)) {
+            o[i] = (uint8_t)sym;
+        } else {
+            acc |= sym << (8 * na);
+            if (++na == 4) {
+                *(uint32_t *)(o + i - 3) = acc;
+                acc = 0;
+                na = 0;
+            }
+        }
+        ++i;
     }
+    for (uint32_t k = 0; k < na; ++k) o[i - na + k] = (uint8_t)(acc >> (8 * k));
     // the block's last segment must have produced exactly n symbols in total
     if (g + 1 == B.seg0 + B.nseg && i < B.n) atomicOr(status, 1u);
 }
@@ -618,6 +715,7 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
         B.seg0 = (uint32_t)seg_block.size();
         B.nseg = tabs[b].single ? 0u : (uint32_t)((B.pay_bits + kSegBits - 1) / kSegBits);
         seg_block.insert(seg_block.end(), B.nseg, b);
+        seg_block.resize((seg_block.size() + 255) & ~(size_t)255, kNil);  // workgroups stay in one block
         B.sp0 = (uint32_t)sp_block.size();
         B.nsp = (uint32_t)((n + kSplit - 1) / kSplit) + 1;
         sp_block.insert(sp_block.end(), B.nsp, b);
@@ -666,7 +764,7 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
         BMH_LAUNCH(c, "dec_huff_pass1", k_hd_pass1, cdiv(nseg, 256), 256, 0, d_blk, d_tab, d_seg_block, nseg, d_end,
                    d_cnt, d_bnd);
         // pass-1 starts are the nominal segment starts
-        std::vector<uint64_t> st0(nseg);
+        std::vector<uint64_t> st0(nseg, 0);
         for (uint32_t b = 0; b < nb; ++b)
             for (uint32_t k = 0; k < hb[b].nseg; ++k) st0[hb[b].seg0 + k] = (uint64_t)k * kSegBits;
         c->h2d(d_start, st0.data(), nseg * 8);
