@@ -507,9 +507,22 @@ __global__ __launch_bounds__(256) void k_lf_scan(const DBlock *__restrict__ blks
 // Stable ranks inside a chunk: wave w owns rows [1024w, 1024w + 1024) in 16 steps of 64; a
 // row's rank among equal bytes of its step comes from 8 ballots, the counts of earlier steps
 // and waves from LDS. Output E[r] = LF(r) | L[r] << 32.
+// E[r] = LF(r) and L[r] in one word: u32 (LF < 2^24) when every block is <= 16 MiB, else u64
+template <typename ET> __device__ __forceinline__ ET make_e(uint32_t lf, uint32_t l);
+template <> __device__ __forceinline__ uint32_t make_e<uint32_t>(uint32_t lf, uint32_t l) { return lf | (l << 24); }
+template <> __device__ __forceinline__ uint64_t make_e<uint64_t>(uint32_t lf, uint32_t l)
+{
+    return lf | ((uint64_t)l << 32);
+}
+__device__ __forceinline__ uint32_t e_lf(uint32_t e) { return e & 0xffffffu; }
+__device__ __forceinline__ uint32_t e_lf(uint64_t e) { return (uint32_t)e; }
+__device__ __forceinline__ uint32_t e_l(uint32_t e) { return e >> 24; }
+__device__ __forceinline__ uint32_t e_l(uint64_t e) { return (uint32_t)(e >> 32); }
+
+template <typename ET>
 __global__ __launch_bounds__(256) void k_lf_rank(const uint8_t *__restrict__ L, const DBlock *__restrict__ blks,
                                                  const uint32_t *__restrict__ ch_block,
-                                                 const uint32_t *__restrict__ chist, uint64_t *__restrict__ E)
+                                                 const uint32_t *__restrict__ chist, ET *__restrict__ E)
 {
     __shared__ uint32_t s_wcnt[4][256];
     const uint32_t c = blockIdx.x, b = ch_block[c];
@@ -548,12 +561,12 @@ __global__ __launch_bounds__(256) void k_lf_rank(const uint8_t *__restrict__ L, 
     }
     __syncthreads();
     const uint32_t *cb = chist + (size_t)c * 256;
-    uint64_t *Eb = E + B.out_off + r0;
+    ET *Eb = E + B.out_off + r0;
     for (uint32_t it = 0; it < 16; ++it) {
         const uint32_t r = 1024 * w + 64 * it + lane;
         if (r < len) {
             const uint32_t x = sym[it];
-            Eb[r] = (uint64_t)(cb[x] + s_wcnt[w][x] + rk[it]) | ((uint64_t)x << 32);
+            Eb[r] = make_e<ET>(cb[x] + s_wcnt[w][x] + rk[it], x);
         }
     }
 }
@@ -569,10 +582,16 @@ __device__ __forceinline__ uint32_t split_row(uint32_t id, const DBlock &B)
     return id * kSplit < B.n ? id * kSplit : B.primary;
 }
 
-// walk 1: each splitter follows LF to the next splitter; the list is cut before the primary
+// walk 1: each splitter follows LF to the next splitter (the list is cut before the primary),
+// writing the first kSlot characters of its segment into its slot of `tmp` and remembering
+// the row reached after kSlot steps, so only segments longer than kSlot are walked again.
+constexpr uint32_t kSlot = 1024;
+
+template <typename ET>
 __global__ __launch_bounds__(256) void k_lf_walk1(const DBlock *__restrict__ blks, const uint32_t *__restrict__ sp_block,
-                                                  uint32_t nsp_total, const uint64_t *__restrict__ E,
+                                                  uint32_t nsp_total, const ET *__restrict__ E,
                                                   uint32_t *__restrict__ nxt, uint64_t *__restrict__ dist,
+                                                  uint32_t *__restrict__ resume, uint8_t *__restrict__ tmp,
                                                   uint32_t *status)
 {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
@@ -586,13 +605,25 @@ __global__ __launch_bounds__(256) void k_lf_walk1(const DBlock *__restrict__ blk
         dist[g] = 0;
         return;
     }
-    const uint64_t *Eb = E + B.out_off;
-    uint32_t r = r0, len = 0, sid;
+    const ET *Eb = E + B.out_off;
+    uint8_t *slot = tmp + (size_t)g * kSlot;
+    uint32_t r = r0, len = 0, sid, acc = 0;
     do {
-        r = (uint32_t)Eb[r];
+        const ET e = Eb[r];
+        if (len < kSlot) {
+            acc |= e_l(e) << (8 * (len & 3u));
+            if ((len & 3u) == 3u) {
+                *(uint32_t *)(slot + len - 3) = acc;
+                acc = 0;
+            }
+        } else if (len == kSlot) {
+            resume[g] = r;
+        }
+        r = e_lf(e);
         ++len;
         sid = split_id(r, B);
     } while (sid == kNil && len <= B.n);
+    if (len < kSlot && (len & 3u)) *(uint32_t *)(slot + (len & ~3u)) = acc;
     if (len > B.n || r >= B.n) {
         atomicOr(status, 2u);
         sid = kNil;
@@ -619,12 +650,69 @@ __global__ __launch_bounds__(256) void k_lf_jump(uint32_t nsp_total, const uint3
     if (nxt_in[nx] != kNil) atomicOr(more, 1u);
 }
 
-// walk 2: splitter g writes its segment; the segment starting at row r covers text positions
-// dist[g] - 1 down to dist[g] - len (the text comes out of LF backwards)
-__global__ __launch_bounds__(256) void k_lf_walk2(const DBlock *__restrict__ blks, const uint32_t *__restrict__ sp_block,
-                                                  uint32_t nsp_total, const uint64_t *__restrict__ E,
+// pointer jumping of one block's splitter list in LDS (blocks with <= kJumpLds splitters)
+constexpr uint32_t kJumpLds = 16385, kJumpNT = 1024, kJumpIPT = (kJumpLds + kJumpNT - 1) / kJumpNT;
+
+__global__ __launch_bounds__(kJumpNT) void k_lf_jump_lds(const DBlock *__restrict__ blks, uint32_t *__restrict__ nxt,
+                                                         uint64_t *__restrict__ dist)
+{
+    __shared__ uint16_t s_nx[kJumpLds];
+    __shared__ uint32_t s_d[kJumpLds];
+    __shared__ int s_more;
+    const DBlock B = blks[blockIdx.x];
+    const uint32_t t = threadIdx.x, m = B.nsp;
+    for (uint32_t i = t; i < m; i += kJumpNT) {
+        const uint32_t x = nxt[B.sp0 + i];
+        s_nx[i] = x == kNil ? 0xffffu : (uint16_t)(x - B.sp0);
+        s_d[i] = (uint32_t)dist[B.sp0 + i];
+    }
+    for (int round = 0; round < 40; ++round) {
+        if (t == 0) s_more = 0;
+        __syncthreads();
+        uint32_t nn[kJumpIPT], dd[kJumpIPT];
+        bool any = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kJumpIPT; ++k) {
+            const uint32_t i = t + k * kJumpNT;
+            nn[k] = 0xffffu;
+            if (i < m) {
+                const uint32_t x = s_nx[i];
+                dd[k] = s_d[i];
+                if (x != 0xffffu) {
+                    nn[k] = s_nx[x];
+                    dd[k] += s_d[x];
+                    any |= nn[k] != 0xffffu;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < kJumpIPT; ++k) {
+            const uint32_t i = t + k * kJumpNT;
+            if (i < m) {
+                s_nx[i] = (uint16_t)nn[k];
+                s_d[i] = dd[k];
+            }
+        }
+        if (any) s_more = 1;
+        __syncthreads();
+        if (!s_more) break;
+    }
+    for (uint32_t i = t; i < m; i += kJumpNT) {
+        nxt[B.sp0 + i] = s_nx[i] == 0xffffu ? kNil : B.sp0 + s_nx[i];
+        dist[B.sp0 + i] = s_d[i];
+    }
+}
+
+// place: splitter g copies its segment from its slot to text positions dist[g] - 1 down to
+// dist[g] - len (the text comes out of LF backwards); past kSlot it walks on from `resume`.
+template <typename ET>
+__global__ __launch_bounds__(256) void k_lf_place(const DBlock *__restrict__ blks, const uint32_t *__restrict__ sp_block,
+                                                  uint32_t nsp_total, const ET *__restrict__ E,
                                                   const uint64_t *__restrict__ dist, const uint32_t *__restrict__ nxt,
-                                                  uint8_t *__restrict__ out, uint32_t *status)
+                                                  const uint32_t *__restrict__ resume, const uint8_t *__restrict__ tmp,
+                                                  const uint64_t *__restrict__ len_of, uint8_t *__restrict__ out,
+                                                  uint32_t *status)
 {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= nsp_total) return;
@@ -634,19 +722,24 @@ __global__ __launch_bounds__(256) void k_lf_walk2(const DBlock *__restrict__ blk
     if (id * kSplit >= B.n && B.primary % kSplit == 0) return;
     // a periodic text (u^k) has k LF cycles; only the primary's one is written (see k_lf_period)
     if (nxt[g] != kNil) return;
-    const uint64_t *Eb = E + B.out_off;
     uint8_t *ob = out + B.out_off;
-    uint64_t pos = dist[g];
-    uint32_t r = split_row(id, B);
-    if (pos > B.n) {
+    const uint64_t pos = dist[g], len = len_of[g];
+    if (pos > B.n || len > pos) {
         atomicOr(status, 2u);
         return;
     }
-    do {
-        const uint64_t e = Eb[r];
-        ob[--pos] = (uint8_t)(e >> 32);
-        r = (uint32_t)e;
-    } while (split_id(r, B) == kNil && pos > 0);
+    const uint8_t *slot = tmp + (size_t)g * kSlot;
+    const uint64_t inslot = len < kSlot ? len : kSlot;
+    for (uint64_t t = 0; t < inslot; ++t) ob[pos - 1 - t] = slot[t];
+    if (len > kSlot) {
+        const ET *Eb = E + B.out_off;
+        uint32_t r = resume[g];
+        for (uint64_t t = kSlot; t < len; ++t) {
+            const ET e = Eb[r];
+            ob[pos - 1 - t] = (uint8_t)e_l(e);
+            r = e_lf(e);
+        }
+    }
 }
 
 // grid = nblocks: if the primary's LF cycle is shorter than n, the text is u^k with |u| = p;
@@ -673,6 +766,55 @@ __global__ __launch_bounds__(64) void k_gather_headers(const uint8_t *__restrict
     const uint32_t b = blockIdx.x;
     const uint64_t o = offs[b], len = offs[b + 1] - o;
     for (uint32_t i = threadIdx.x; i < 352; i += 64) hdr[(size_t)b * 352 + i] = i < len ? rec[o + i] : 0;
+}
+
+}  // namespace
+
+namespace {
+
+// LF by stable counting sort, one LF-cycle walk that stages each segment in a slot, a
+// pointer-jumping ranking of the splitters, and a placement pass.
+template <typename ET>
+void lf_inverse(Ctx *c, const std::vector<DBlock> &hb, uint32_t nb, uint64_t total, uint32_t nsp, uint32_t nch,
+                uint32_t max_nsp, const uint8_t *d_L, const DBlock *d_blk, const uint32_t *d_ch_block,
+                const uint32_t *d_sp_block, uint8_t *d_out, uint32_t *d_status)
+{
+    uint32_t *d_chist = (uint32_t *)c->get(WS_BSTART, (size_t)nch * 256 * 4 + 64);
+    ET *d_E = (ET *)c->get(WS_KEY8, total * sizeof(ET) + 64);
+    BMH_LAUNCH(c, "dec_lf_hist", k_lf_hist, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist);
+    BMH_LAUNCH(c, "dec_lf_scan", k_lf_scan, nb, 256, 0, d_blk, d_chist);
+    BMH_LAUNCH(c, "dec_lf_rank", k_lf_rank<ET>, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist, d_E);
+    uint8_t *d_sp = (uint8_t *)c->get(WS_RKA, (size_t)nsp * 36 + 64);
+    uint32_t *d_nxt = (uint32_t *)d_sp, *d_nxt2 = d_nxt + nsp, *d_resume = d_nxt2 + nsp;
+    uint64_t *d_dist = (uint64_t *)(((uintptr_t)(d_resume + nsp) + 7) & ~(uintptr_t)7), *d_dist2 = d_dist + nsp;
+    uint64_t *d_len = (uint64_t *)c->get(WS_RKB, (size_t)nsp * 8 + 64);
+    uint8_t *d_tmp = (uint8_t *)c->get(WS_KEY, (size_t)nsp * kSlot + 64);
+    BMH_LAUNCH(c, "dec_lf_walk", k_lf_walk1<ET>, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, nsp, d_E, d_nxt, d_dist,
+               d_resume, d_tmp, d_status);
+    BMH_HIP(hipMemcpyAsync(d_len, d_dist, (size_t)nsp * 8, hipMemcpyDeviceToDevice, c->stream));
+    // pointer jumping until the primary's chain is ranked; splitters on other LF cycles
+    // (periodic text) never reach the cut, so the rounds are bounded by log2(splitters)
+    if (max_nsp <= kJumpLds) {
+        BMH_LAUNCH(c, "dec_lf_jump", k_lf_jump_lds, nb, kJumpNT, 0, d_blk, d_nxt, d_dist);
+    } else {
+        uint32_t *d_more = d_status + 2;
+        int rounds = 1;
+        while ((1u << rounds) < max_nsp) ++rounds;
+        for (int round = 0; round <= rounds; ++round) {
+            BMH_HIP(hipMemsetAsync(d_more, 0, 4, c->stream));
+            BMH_LAUNCH(c, "dec_lf_jump", k_lf_jump, cdiv(nsp, 256), 256, 0, nsp, d_nxt, d_dist, d_nxt2, d_dist2,
+                       d_more);
+            std::swap(d_nxt, d_nxt2);
+            std::swap(d_dist, d_dist2);
+            uint32_t more = 0;
+            c->d2h(&more, d_more, 4);
+            c->sync();
+            if (!more) break;
+        }
+    }
+    BMH_LAUNCH(c, "dec_lf_place", k_lf_place<ET>, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, nsp, d_E, d_dist, d_nxt,
+               d_resume, d_tmp, d_len, d_out, d_status);
+    BMH_LAUNCH(c, "dec_lf_period", k_lf_period, nb, 256, 0, d_blk, d_dist, d_out, d_status);
 }
 
 }  // namespace
@@ -793,36 +935,16 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
     BMH_LAUNCH(c, "dec_imtf", k_imtf<1>, cdiv(nch, kImtfLanes), kImtfLanes, 0, d_mtf, d_ich, nch, d_S, d_L);
 
     // ---- BWT^-1 -> d_out
-    uint32_t *d_chist = (uint32_t *)c->get(WS_BSTART, (size_t)nch * 256 * 4 + 64);
-    uint64_t *d_E = (uint64_t *)c->get(WS_KEY8, total * 8 + 64);
-    BMH_LAUNCH(c, "dec_lf_hist", k_lf_hist, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist);
-    BMH_LAUNCH(c, "dec_lf_scan", k_lf_scan, nb, 256, 0, d_blk, d_chist);
-    BMH_LAUNCH(c, "dec_lf_rank", k_lf_rank, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist, d_E);
-    uint8_t *d_sp = (uint8_t *)c->get(WS_RKA, (size_t)nsp * 24 + 64);
-    uint32_t *d_nxt = (uint32_t *)d_sp, *d_nxt2 = d_nxt + nsp;
-    uint64_t *d_dist = (uint64_t *)(((uintptr_t)(d_nxt2 + nsp) + 7) & ~(uintptr_t)7), *d_dist2 = d_dist + nsp;
-    BMH_LAUNCH(c, "dec_lf_walk1", k_lf_walk1, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, nsp, d_E, d_nxt, d_dist,
-               d_status);
-    // pointer jumping until the primary's chain is ranked; splitters on other LF cycles
-    // (periodic text) never reach the cut, so the rounds are bounded by log2(splitters)
-    uint32_t *d_more = d_status + 2;
+    bool small = true;
     uint32_t max_nsp = 1;
-    for (uint32_t b = 0; b < nb; ++b) max_nsp = std::max(max_nsp, hb[b].nsp);
-    int rounds = 1;
-    while ((1u << rounds) < max_nsp) ++rounds;
-    for (int round = 0; round <= rounds; ++round) {
-        BMH_HIP(hipMemsetAsync(d_more, 0, 4, c->stream));
-        BMH_LAUNCH(c, "dec_lf_jump", k_lf_jump, cdiv(nsp, 256), 256, 0, nsp, d_nxt, d_dist, d_nxt2, d_dist2, d_more);
-        std::swap(d_nxt, d_nxt2);
-        std::swap(d_dist, d_dist2);
-        uint32_t more = 0;
-        c->d2h(&more, d_more, 4);
-        c->sync();
-        if (!more) break;
+    for (uint32_t b = 0; b < nb; ++b) {
+        small &= hb[b].n <= (1u << 24);
+        max_nsp = std::max(max_nsp, hb[b].nsp);
     }
-    BMH_LAUNCH(c, "dec_lf_walk2", k_lf_walk2, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, nsp, d_E, d_dist, d_nxt,
-               d_out, d_status);
-    BMH_LAUNCH(c, "dec_lf_period", k_lf_period, nb, 256, 0, d_blk, d_dist, d_out, d_status);
+    if (small)
+        lf_inverse<uint32_t>(c, hb, nb, total, nsp, nch, max_nsp, d_L, d_blk, d_ch_block, d_sp_block, d_out, d_status);
+    else
+        lf_inverse<uint64_t>(c, hb, nb, total, nsp, nch, max_nsp, d_L, d_blk, d_ch_block, d_sp_block, d_out, d_status);
     uint32_t st = 0;
     c->d2h(&st, d_status, 4);
     c->sync();
