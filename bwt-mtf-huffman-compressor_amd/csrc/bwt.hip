@@ -43,6 +43,7 @@ constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kFinNT = 256, kFinCap = 4096;
 constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
+constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
 constexpr uint32_t kDataMaxBits = 64;           // deeper MSD ties go to rank doubling
 constexpr uint32_t kFinMaxBits = 256;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
@@ -56,7 +57,7 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t fin_next, big_next, big, dgroups, dmin_bits, pad0, pad1, pad2;  // data phase
+    uint32_t fin_next, fint_next, finb_next, big_next, big, dgroups, dmin_bits, pad0;  // data phase
 };
 
 // Data-phase segment / group: {gstart (batch slot), len, bit depth, block (| kFinalFlag)}
@@ -82,7 +83,9 @@ struct DataArgs {
     uint32_t *prim;
     uint32_t *bflag;   // block keeps tied groups -> needs the rank phase
     Seg4 *groups;      // tied groups (unresolved or final)
-    Seg4 *fin_next;    // deferred finish segments
+    Seg4 *fin_next;    // deferred finish segments, 64 < len <= kFinCap
+    Seg4 *fint_next;   // deferred finish segments, len <= kTinyFin
+    Seg4 *finb_next;   // deferred finish segments, len > kFinCap
     Seg4 *big_next;    // MSD segments for the next pass
     Counters *cnt;
 };
@@ -128,7 +131,18 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
     return w;
 }
 
-// A tied run of m > kSmallM rotations, grouped up to bit depth nd: another finish pass, or
+// A list segment for the next finish round, by size class (each class has its own kernel).
+__device__ __forceinline__ void push_fin(const DataArgs &a, Seg4 sg)
+{
+    if (sg.y <= kTinyFin)
+        a.fint_next[atomicAdd(&a.cnt->fint_next, 1u)] = sg;
+    else if (sg.y <= kFinCap)
+        a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = sg;
+    else
+        a.finb_next[atomicAdd(&a.cnt->finb_next, 1u)] = sg;
+}
+
+// A tied run of m rotations, grouped up to bit depth nd: another finish pass, or
 // rank doubling once it is deep (long repeats), or final when nd covers the whole rotation.
 __device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, uint32_t m, uint32_t nd, uint32_t b,
                                               uint32_t n)
@@ -139,7 +153,7 @@ __device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, ui
         a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, m, nd, b);
         a.bflag[b] = 1;
     } else {
-        a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gs, m, nd, b);
+        push_fin(a, make_uint4(gs, m, nd, b));
     }
 }
 
@@ -231,7 +245,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     if (run > kBigCap)
         big[atomicAdd(&cnt->big, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[atomicAdd(&cnt->fin_next, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        fin[atomicAdd(&cnt->finb_next, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -453,6 +467,43 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
     __syncthreads();
 }
 
+// Tiny list segments (len <= kTinyFin): one wave each, lane = element, ranked by the next 64
+// rotation bits with wave shuffles (tie groups of 2-3 rotations are the common case).
+__global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list, uint32_t nlist)
+{
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    const uint32_t i = blockIdx.x * 4 + w;
+    if (i >= nlist) return;  // the whole wave
+    const Seg4 sg = list[i];
+    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    uint32_t p = 0;
+    uint64_t key = ~0ull;
+    if (l < len) {
+        p = a.sa[gstart + l];
+        key = rot_window(blk, n, p, db);
+    }
+    uint32_t lt = 0, eqb = 0, eqt = 0;
+    for (uint32_t j = 0; j < len; ++j) {
+        const uint32_t klo = __shfl((uint32_t)key, (int)j, 64), khi = __shfl((uint32_t)(key >> 32), (int)j, 64);
+        const uint64_t kj = ((uint64_t)khi << 32) | klo;
+        lt += kj < key;
+        eqt += kj == key;
+        eqb += kj == key && j < l;
+    }
+    if (l >= len) return;
+    const uint64_t newbits = (uint64_t)db + 64;
+    const bool final_depth = newbits >= 8ull * n;
+    const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
+    if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+    a.sa[slot] = p;
+    if (eqt == 1 || final_depth) {
+        a.L[slot] = lastcol_byte(blk, n, p);
+        if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+    }
+}
+
 // List segments (lo < len <= CAP) at any depth: rotation windows gathered from the text.
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
@@ -572,7 +623,7 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
             a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u));
             if (!final_depth) a.bflag[b] = 1;
         } else if (len <= kBigCap) {
-            a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = make_uint4(gs, len, nd, b);
+            push_fin(a, make_uint4(gs, len, nd, b));
         } else {
             a.big_next[atomicAdd(&a.cnt->big_next, 1u)] = make_uint4(gs, len, nd, b);
         }
@@ -1167,8 +1218,13 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list
-    Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, seg_cap * 16);
-    Seg4 *fin_nxt = (Seg4 *)c->get(WS_FIN_NXT, seg_cap * 16);
+    // finish lists by size class; every entry covers > kTinyFin / > kFinCap positions
+    Seg4 *fint_cur = (Seg4 *)c->get(WS_FINT_CUR, seg_cap * 16);
+    Seg4 *fint_nxt = (Seg4 *)c->get(WS_FINT_NXT, seg_cap * 16);
+    Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, (N / (kTinyFin + 1) + 2) * 16);
+    Seg4 *fin_nxt = (Seg4 *)c->get(WS_FIN_NXT, (N / (kTinyFin + 1) + 2) * 16);
+    Seg4 *finb_cur = (Seg4 *)c->get(WS_FINB_CUR, (N / (kFinCap + 1) + 2) * 16);
+    Seg4 *finb_nxt = (Seg4 *)c->get(WS_FINB_NXT, (N / (kFinCap + 1) + 2) * 16);
     Seg4 *dgroups = (Seg4 *)c->get(WS_GROUPS, seg_cap * 16);
     Seg4 *big = (Seg4 *)c->get(WS_LARGE, (N / kFinCap + 2) * 16);
     Seg4 *big2 = (Seg4 *)c->get(WS_LARGE2, (N / kFinCap + 2) * 16);
@@ -1198,29 +1254,33 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     // ---- data phase
     BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, fin_cur, big,
+    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, finb_cur, big,
                d_cnt);
     BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
     // the dense finish appends deferred segments after the global pass's list entries
     da.fin_next = fin_cur;
+    da.fint_next = fint_cur;
+    da.finb_next = finb_cur;
     da.big_next = big2;
     BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
                da, bk, rec);
     read_counters();
-    uint32_t nfin = h_cnt->fin_next, nbig = h_cnt->big;
+    uint32_t nfin = h_cnt->fin_next, nfint = h_cnt->fint_next, nfinb = h_cnt->finb_next, nbig = h_cnt->big;
     Seg4 *big_cur = big, *big_nxt = big2;
     std::vector<Seg4> hs;
     std::vector<DTile> ht;
     std::vector<uint2> hst;
-    while (nfin > 0 || nbig > 0) {
-        BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 8, c->stream));  // fin_next, big_next
-        // finish segments first (they write fin_next -> other buffer)
-        if (nfin > 0) {
-            da.fin_next = fin_nxt;
-            da.big_next = big_nxt;
-            BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
-            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfin, kBigNT, 0, da, fin_cur, kFinCap);
-        }
+    while (nfin > 0 || nfint > 0 || nfinb > 0 || nbig > 0) {
+        BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 16, c->stream));  // fin_next, fint_next, finb_next, big_next
+        // every pass of a round writes the other buffer of each list
+        da.fin_next = fin_nxt;
+        da.fint_next = fint_nxt;
+        da.finb_next = finb_nxt;
+        da.big_next = big_nxt;
+        if (nfint > 0) BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4), 256, 0, da, fint_cur, nfint);
+        if (nfin > 0) BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
+        if (nfinb > 0)
+            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfinb, kBigNT, 0, da, finb_cur, kFinCap);
         if (nbig > 0) {
             hs.resize(nbig);
             c->d2h(hs.data(), big_cur, nbig * sizeof(Seg4));
@@ -1245,8 +1305,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         }
         read_counters();
         nfin = h_cnt->fin_next;
+        nfint = h_cnt->fint_next;
+        nfinb = h_cnt->finb_next;
         nbig = h_cnt->big_next;
         std::swap(fin_cur, fin_nxt);
+        std::swap(fint_cur, fint_nxt);
+        std::swap(finb_cur, finb_nxt);
         std::swap(big_cur, big_nxt);
     }
 

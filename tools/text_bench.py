@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Encode throughput on Zipf text — configs 3 (100 MB, 1 MiB blocks) and 5
+(16 MiB blocks) — with the per-kernel breakdown. usage: python tools/text_bench.py [MB] [block_MiB]"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "bwt-mtf-huffman-compressor_amd"))
+import bmh  # noqa: E402
+from bmh import synth  # noqa: E402
+
+mb = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+bs = (int(sys.argv[2]) if len(sys.argv) > 2 else 1) << 20
+n = mb * 1000 * 1000
+z = synth.zipf_text(n)
+ctx = bmh.Context(0)
+nb = (n + bs - 1) // bs
+offs = np.minimum(np.arange(nb + 1, dtype=np.uint64) * np.uint64(bs), np.uint64(n))
+d_in = ctx.alloc(n)
+d_in.upload(z)
+cap = sum(int(bmh.lib().bmh_record_bound(int(offs[i + 1] - offs[i]))) for i in range(nb))
+d_out = ctx.alloc(cap)
+ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)  # warm-up
+t0 = time.perf_counter()
+steps = 3
+for _ in range(steps):
+    ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+dt = (time.perf_counter() - t0) / steps
+os.environ["BMH_STREAMS"] = "1"
+ctx.reset_stats()
+ctx.set_timing(True)
+ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+st = ctx.kernel_stats()
+ctx.set_timing(False)
+res = {"MB": mb, "block_MiB": bs >> 20, "blocks": nb, "ms": round(dt * 1e3, 2), "MBps": round(n / dt / 1e6, 1),
+       "ratio": round(float(ro[-1]) / n, 6),
+       "kernels_ms": {k: [v[0], round(v[1], 2)] for k, v in sorted(st.items(), key=lambda kv: -kv[1][1])[:16]}}
+man = os.path.join(REPO, "tests", "golden", "manifests", "zipf100m_1m.json")
+if mb == 100 and bs == 1 << 20 and os.path.exists(man):
+    recs = d_out.download(int(ro[-1]))
+    agg = hashlib.sha256(recs.tobytes()).hexdigest()
+    res["parity"] = agg == json.load(open(man))["aggregate_sha256"]
+print(json.dumps(res))
