@@ -30,7 +30,7 @@ namespace bmh {
 namespace {
 
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
-constexpr int kLanes = 256;           // lanes (chunks) per encode workgroup
+constexpr int kLanes = 128;           // lanes (chunks) per encode workgroup
 constexpr int kMtfGroup = 2;          // symbols per batched MTF step
 
 struct MChunk {
