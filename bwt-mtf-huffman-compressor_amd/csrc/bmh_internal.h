@@ -79,6 +79,9 @@ struct Ctx {
     // sub-pipelines (own stream + workspaces) a batch is split across (capi.cpp)
     std::vector<Ctx *> subs;
     int nstreams = 0;  // 0: BMH_STREAMS or the default
+    // BWT: write the suffix array of every slot (needed by rank doubling) instead of only the
+    // slots later passes read; set after a batch needed doubling, cleared when one did not
+    bool bwt_full_sa = false;
 
     void *get(Slot s, size_t bytes);
     void *host_pinned(size_t bytes);

@@ -45,8 +45,9 @@ constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
 constexpr uint32_t kDataMaxBits = 64;           // deeper MSD ties go to rank doubling
-constexpr uint32_t kFinMaxBits = 256;           // deeper finish-pass ties go to rank doubling
+constexpr uint32_t kFinMaxBits = 512;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
+constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries per workgroup
 // doubling phase
 constexpr uint32_t kTinyMax = 128;
 constexpr uint32_t kTileT = 1024;
@@ -57,7 +58,7 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t fin_next, fint_next, finb_next, big_next, big, dgroups, dmin_bits, pad0;  // data phase
+    uint32_t fin_next, fint_next, finb_next, big_next, big, dgroups, dmin_bits, flagged;  // data phase
 };
 
 // Data-phase segment / group: {gstart (batch slot), len, bit depth, block (| kFinalFlag)}
@@ -88,6 +89,7 @@ struct DataArgs {
     Seg4 *finb_next;   // deferred finish segments, len > kFinCap
     Seg4 *big_next;    // MSD segments for the next pass
     Counters *cnt;
+    uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
 };
 
 __device__ __forceinline__ uint8_t lastcol_byte(const uint8_t *blk, uint32_t n, uint32_t p)
@@ -131,30 +133,102 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
     return w;
 }
 
-// A list segment for the next finish round, by size class (each class has its own kernel).
-__device__ __forceinline__ void push_fin(const DataArgs &a, Seg4 sg)
+// The lists a deferred segment can go to.
+enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListGroups = 3, kListBig = 4, kNumLists = 5 };
+
+__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l)
 {
-    if (sg.y <= kTinyFin)
-        a.fint_next[atomicAdd(&a.cnt->fint_next, 1u)] = sg;
-    else if (sg.y <= kFinCap)
-        a.fin_next[atomicAdd(&a.cnt->fin_next, 1u)] = sg;
-    else
-        a.finb_next[atomicAdd(&a.cnt->finb_next, 1u)] = sg;
+    switch (l) {
+    case kListTiny: return &a.cnt->fint_next;
+    case kListFin: return &a.cnt->fin_next;
+    case kListFinb: return &a.cnt->finb_next;
+    case kListGroups: return &a.cnt->dgroups;
+    default: return &a.cnt->big_next;
+    }
 }
 
-// A tied run of m rotations, grouped up to bit depth nd: another finish pass, or
-// rank doubling once it is deep (long repeats), or final when nd covers the whole rotation.
-__device__ __forceinline__ void defer_segment(const DataArgs &a, uint32_t gs, uint32_t m, uint32_t nd, uint32_t b,
-                                              uint32_t n)
+__device__ __forceinline__ Seg4 *list_base(const DataArgs &a, uint32_t l)
 {
-    if (nd >= 8ull * n) {
-        a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, m, nd, b | kFinalFlag);
-    } else if (nd >= kFinMaxBits) {
-        a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, m, nd, b);
-        a.bflag[b] = 1;
-    } else {
-        push_fin(a, make_uint4(gs, m, nd, b));
+    switch (l) {
+    case kListTiny: return a.fint_next;
+    case kListFin: return a.fin_next;
+    case kListFinb: return a.finb_next;
+    case kListGroups: return a.groups;
+    default: return a.big_next;
     }
+}
+
+// A tied run of m rotations, grouped up to bit depth nd (sg = {gs, m, nd, b}): another finish
+// pass by size class, or rank doubling once it is deep (long repeats), or final when nd
+// covers the whole rotation (block flag in sg.w).
+__device__ __forceinline__ uint32_t defer_list(const DataArgs &a, Seg4 &sg, uint32_t n)
+{
+    if (sg.z >= 8ull * n) {
+        sg.w |= kFinalFlag;
+        return kListGroups;
+    }
+    if (sg.z >= kFinMaxBits) {
+        a.bflag[sg.w] = 1;
+        a.cnt->flagged = 1;
+        return kListGroups;
+    }
+    return sg.y <= kTinyFin ? kListTiny : sg.y <= kFinCap ? kListFin : kListFinb;
+}
+
+// Deferred segments queued per workgroup in LDS; one global atomic per list reserves the
+// workgroup's entries at the flush. (Single-entry pushes from every workgroup onto the same
+// few counters serialise at the L2: on text, millions of them cost tens of ms per round.)
+template <uint32_t Q>
+struct DeferQueue {
+    uint32_t n;                  // entries pushed (beyond Q they went to the lists directly)
+    uint32_t cnt[kNumLists], base[kNumLists];
+    Seg4 e[Q];
+    uint32_t tag[Q];             // list << 24 | index inside the list's reservation
+};
+
+// before the first push; a barrier must separate it from the pushes
+template <uint32_t Q>
+__device__ __forceinline__ void dq_init(DeferQueue<Q> &q)
+{
+    if (threadIdx.x < kNumLists) q.cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) q.n = 0;
+}
+
+template <uint32_t Q>
+__device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q, Seg4 sg, uint32_t l)
+{
+    const uint32_t i = atomicAdd(&q.n, 1u);
+    if (i < Q) {
+        q.e[i] = sg;
+        q.tag[i] = (l << 24) | atomicAdd(&q.cnt[l], 1u);
+    } else {
+        list_base(a, l)[atomicAdd(list_counter(a, l), 1u)] = sg;
+    }
+}
+
+template <uint32_t Q>
+__device__ __forceinline__ void dq_push(const DataArgs &a, DeferQueue<Q> &q, uint32_t gs, uint32_t m, uint32_t nd,
+                                        uint32_t b, uint32_t n)
+{
+    Seg4 sg = make_uint4(gs, m, nd, b);
+    const uint32_t l = defer_list(a, sg, n);
+    dq_push_list(a, q, sg, l);
+}
+
+// all threads, once per queue; starts and ends with a barrier
+template <uint32_t NT, uint32_t Q>
+__device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
+{
+    __syncthreads();
+    const uint32_t t = threadIdx.x;
+    if (t < kNumLists && q.cnt[t]) q.base[t] = atomicAdd(list_counter(a, t), q.cnt[t]);
+    __syncthreads();
+    const uint32_t qn = min(q.n, Q);
+    for (uint32_t i = t; i < qn; i += NT) {
+        const uint32_t tg = q.tag[i], l = tg >> 24;
+        list_base(a, l)[q.base[l] + (tg & 0xffffffu)] = q.e[i];
+    }
+    __syncthreads();
 }
 
 // Compact rotation record the global pass writes for dense buckets (u64): rotation bits
@@ -336,7 +410,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
             const uint32_t P = rec_pbits(n), R = rec_rbits(P);
             const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
             rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
-        } else
+        } else if (blen > 1 || a.full_sa)
             a.sa[boff + slot] = p;
         if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
@@ -365,13 +439,14 @@ struct FinishShape {
 
 // The finish of one segment once every element is in registers: pl = position (<< 8 | last-
 // column byte when packL), dd = 12-bit digit, rv = R-bit rest. s_cnt must be zero on entry
-// and is zero again on return (ends with a barrier).
+// and is zero again on return (ends with a barrier); s_tmp holds NT / 64 + 2 words, the last
+// one zero on entry (set when some slot is deferred: then the segment's SA is stored).
 template <uint32_t NT, uint32_t CAP>
 __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, uint32_t len, uint32_t db, uint32_t b,
                                             uint32_t R, bool packL, uint32_t (&pl)[FinishShape<NT, CAP>::IPT],
                                             uint32_t (&dd)[FinishShape<NT, CAP>::IPT],
                                             uint32_t (&rv)[FinishShape<NT, CAP>::IPT], uint32_t *s_rest,
-                                            uint32_t *s_cnt, uint32_t *s_tmp)
+                                            uint32_t *s_cnt, uint32_t *s_tmp, DeferQueue<kDeferQ> &dq)
 {
     constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT, WPT = FinishShape<NT, CAP>::WPT;
     const uint32_t t = threadIdx.x;
@@ -422,7 +497,10 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         const uint32_t m = s1 - s0;
         if (m > kSmallM) {
             dd[k] = me;  // deferred, grouped by the 12-bit digit
-            if (me == s0) defer_segment(a, gstart + s0, m, db + kSegDigit, b, n);
+            if (me == s0) {
+                dq_push(a, dq, gstart + s0, m, db + kSegDigit, b, n);
+                s_tmp[NT / 64 + 1] = 1;
+            }
             continue;
         }
         uint32_t lt = 0, eqb = 0, eqt = 1;
@@ -439,11 +517,14 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
             }
         }
         const uint32_t local = s0 + lt + eqb, gs = gstart + s0 + lt;
-        if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)newbits, b, n);  // tied so far
+        if (eqt > 1 && eqb == 0) {  // tied so far
+            dq_push(a, dq, gs, eqt, (uint32_t)newbits, b, n);
+            s_tmp[NT / 64 + 1] = 1;
+        }
         dd[k] = local;  // dd now holds the element's slot in the segment
         if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = (eqt == 1 ? gstart + local : gs) - boff;
     }
-    __syncthreads();
+    dq_flush<NT>(a, dq);
     // slot -> position (<< 8 | L); a slot whose rotation is not final yet gets its L
     // rewritten when a later pass resolves it
 #pragma unroll
@@ -451,16 +532,18 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         if (t + k * NT < len) s_rest[dd[k]] = pl[k];
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     __syncthreads();
+    // the SA of a segment nothing defers is never read again (unless rank doubling needs it)
+    const bool wsa = a.full_sa || s_tmp[NT / 64 + 1] != 0;
     if (packL) {
         for (uint32_t i = t; i < len; i += NT) {
             const uint32_t v = s_rest[i];
-            a.sa[gstart + i] = v >> 8;
+            if (wsa) a.sa[gstart + i] = v >> 8;
             a.L[gstart + i] = (uint8_t)v;
         }
     } else {
         for (uint32_t i = t; i < len; i += NT) {
             const uint32_t p = s_rest[i];
-            a.sa[gstart + i] = p;
+            if (wsa) a.sa[gstart + i] = p;
             a.L[gstart + i] = lastcol_byte(blk, n, p);
         }
     }
@@ -468,40 +551,49 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 }
 
 // Tiny list segments (len <= kTinyFin): one wave each, lane = element, ranked by the next 64
-// rotation bits with wave shuffles (tie groups of 2-3 rotations are the common case).
+// rotation bits with wave shuffles (tie groups of 2-3 rotations are the common case). Each
+// wave takes kTinyPerWave segments so that a workgroup's deferrals share one reservation.
+constexpr uint32_t kTinyPerWave = 8;
+
 __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list, uint32_t nlist)
 {
+    __shared__ DeferQueue<kDeferQ> dq;
+    dq_init(dq);
+    __syncthreads();
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-    const uint32_t i = blockIdx.x * 4 + w;
-    if (i >= nlist) return;  // the whole wave
-    const Seg4 sg = list[i];
-    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
-    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-    const uint8_t *blk = a.data + boff;
-    uint32_t p = 0;
-    uint64_t key = ~0ull;
-    if (l < len) {
-        p = a.sa[gstart + l];
-        key = rot_window(blk, n, p, db);
+    for (uint32_t k = 0; k < kTinyPerWave; ++k) {
+        const uint32_t i = (blockIdx.x * kTinyPerWave + k) * 4 + w;
+        if (i >= nlist) break;  // the whole wave
+        const Seg4 sg = list[i];
+        const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
+        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+        const uint8_t *blk = a.data + boff;
+        uint32_t p = 0;
+        uint64_t key = ~0ull;
+        if (l < len) {
+            p = a.sa[gstart + l];
+            key = rot_window(blk, n, p, db);
+        }
+        uint32_t lt = 0, eqb = 0, eqt = 0;
+        for (uint32_t j = 0; j < len; ++j) {
+            const uint32_t klo = __shfl((uint32_t)key, (int)j, 64), khi = __shfl((uint32_t)(key >> 32), (int)j, 64);
+            const uint64_t kj = ((uint64_t)khi << 32) | klo;
+            lt += kj < key;
+            eqt += kj == key;
+            eqb += kj == key && j < l;
+        }
+        if (l >= len) continue;
+        const uint64_t newbits = (uint64_t)db + 64;
+        const bool final_depth = newbits >= 8ull * n;
+        const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
+        if (eqt > 1 && eqb == 0) dq_push(a, dq, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+        a.sa[slot] = p;
+        if (eqt == 1 || final_depth) {
+            a.L[slot] = lastcol_byte(blk, n, p);
+            if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+        }
     }
-    uint32_t lt = 0, eqb = 0, eqt = 0;
-    for (uint32_t j = 0; j < len; ++j) {
-        const uint32_t klo = __shfl((uint32_t)key, (int)j, 64), khi = __shfl((uint32_t)(key >> 32), (int)j, 64);
-        const uint64_t kj = ((uint64_t)khi << 32) | klo;
-        lt += kj < key;
-        eqt += kj == key;
-        eqb += kj == key && j < l;
-    }
-    if (l >= len) return;
-    const uint64_t newbits = (uint64_t)db + 64;
-    const bool final_depth = newbits >= 8ull * n;
-    const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
-    if (eqt > 1 && eqb == 0) defer_segment(a, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
-    a.sa[slot] = p;
-    if (eqt == 1 || final_depth) {
-        a.L[slot] = lastcol_byte(blk, n, p);
-        if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
-    }
+    dq_flush<256>(a, dq);
 }
 
 // List segments (lo < len <= CAP) at any depth: rotation windows gathered from the text.
@@ -511,14 +603,17 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT;
     __shared__ uint32_t s_rest[CAP];
     __shared__ uint32_t s_cnt[FinishShape<NT, CAP>::NDIG / 2];
-    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    __shared__ uint32_t s_tmp[NT / 64 + 2];
+    __shared__ DeferQueue<kDeferQ> dq;
     const Seg4 sg = list[blockIdx.x];
     const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
     if (len <= lo || len > CAP) return;
+    dq_init(dq);
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     const uint32_t t = threadIdx.x;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
+    if (t == 0) s_tmp[NT / 64 + 1] = 0;
     uint32_t pl[IPT], dd[IPT], rv[IPT];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
@@ -531,7 +626,104 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         }
     }
     __syncthreads();
-    finish_core<NT, CAP>(a, gstart, len, db, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp);
+    finish_core<NT, CAP>(a, gstart, len, db, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+}
+
+constexpr uint32_t kSortQ = 1024;  // deferral queue of k_finish_sort (overlays its key array)
+
+// List segments (lo < len <= CAP) sorted by their whole next 64 rotation bits: bitonic sort of
+// (window, position) pairs in LDS, then runs of equal windows become the next round's tie
+// groups at depth db + 64. On text most rotations share several bytes with their neighbours
+// (SURVEY App. D Zipf: median 10, max 44 bytes at 1 MiB blocks), so advancing 64 bits per
+// round instead of 12 takes a block through in ~5 rounds instead of ~20.
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
+{
+    static_assert((CAP & (CAP - 1)) == 0, "bitonic capacity");
+    static_assert(sizeof(DeferQueue<kSortQ>) <= CAP * 8, "deferral queue overlays the windows");
+    __shared__ __align__(16) uint64_t s_key[CAP];
+    __shared__ uint32_t s_pos[CAP];
+    __shared__ uint32_t s_tail[CAP / 32];
+    const Seg4 sg = list[blockIdx.x];
+    const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
+    if (len <= lo || len > CAP) return;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    const uint32_t t = threadIdx.x;
+    const uint32_t M = len <= 2 ? 2u : 1u << (32 - __builtin_clz(len - 1));  // pow2 >= len
+    for (uint32_t i = t; i < M; i += NT) {
+        uint64_t k = ~0ull;
+        uint32_t p = 0xffffffffu;
+        if (i < len) {
+            p = a.sa[gstart + i];
+            k = rot_window(blk, n, p, db);
+        }
+        s_key[i] = k;
+        s_pos[i] = p;
+    }
+    for (uint32_t i = t; i < CAP / 32; i += NT) s_tail[i] = 0;
+    __syncthreads();
+    for (uint32_t k = 2; k <= M; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = t; q < M / 2; q += NT) {
+                const uint32_t i0 = 2 * q - (q & (j - 1)), i1 = i0 + j;
+                const uint64_t k0 = s_key[i0], k1 = s_key[i1];
+                const uint32_t p0 = s_pos[i0], p1 = s_pos[i1];
+                const bool gt = k0 > k1 || (k0 == k1 && p0 > p1);
+                if (gt == ((i0 & k) == 0)) {
+                    s_key[i0] = k1;
+                    s_key[i1] = k0;
+                    s_pos[i0] = p1;
+                    s_pos[i1] = p0;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // runs of equal windows: tails marked in a bitset, each head finds its tail
+    for (uint32_t i = t; i < len; i += NT)
+        if (i + 1 == len || s_key[i + 1] != s_key[i]) atomicOr(&s_tail[i >> 5], 1u << (i & 31u));
+    __syncthreads();
+    const uint64_t newbits = (uint64_t)db + 64;
+    const bool final_depth = newbits >= 8ull * n;
+    constexpr uint32_t IPT = CAP / NT;
+    uint32_t hm[IPT];  // run length at a run head of >= 2 equal windows, else 0
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t i = t + k * NT;
+        hm[k] = 0;
+        if (i >= len) continue;
+        const uint32_t p = s_pos[i];
+        const bool head = i == 0 || s_key[i - 1] != s_key[i];
+        bool single = true;
+        if (!(head && ((s_tail[i >> 5] >> (i & 31u)) & 1u))) {  // part of a tie run
+            single = false;
+            if (head) {
+                uint32_t w = i >> 5, bits = s_tail[w] & (0xffffffffu << (i & 31u));
+                while (bits == 0) bits = s_tail[++w];
+                hm[k] = 32 * w + __builtin_ctz(bits) + 1 - i;
+            }
+        }
+        a.sa[gstart + i] = p;
+        if (single || final_depth) {
+            a.L[gstart + i] = lastcol_byte(blk, n, p);
+            if (p == 0) {
+                uint32_t gs = i;
+                if (!single)
+                    while (gs > 0 && s_key[gs - 1] == s_key[i]) --gs;
+                a.prim[b] = gstart + gs - boff;
+            }
+        }
+    }
+    // the windows are no longer needed: their LDS holds the deferral queue
+    __syncthreads();
+    DeferQueue<kSortQ> &dq = *reinterpret_cast<DeferQueue<kSortQ> *>(s_key);
+    dq_init(dq);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k)
+        if (hm[k]) dq_push(a, dq, gstart + t + k * NT, hm[k], (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+    dq_flush<NT>(a, dq);
 }
 
 // Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
@@ -545,7 +737,8 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT;
     __shared__ uint32_t s_rest[CAP];
     __shared__ uint32_t s_cnt[FinishShape<NT, CAP>::NDIG / 2];
-    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    __shared__ uint32_t s_tmp[NT / 64 + 2];
+    __shared__ DeferQueue<kDeferQ> dq;
     const uint32_t x = blockIdx.x & 7u, kb = blockIdx.x >> 3;
     const uint32_t b = x + 8u * (kb >> kG1Bits);
     if (b >= a.nb) return;
@@ -556,6 +749,8 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     const uint32_t P = rec_pbits(n), R = rec_rbits(P);
     const bool packL = P <= 24;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
+    if (t == 0) s_tmp[NT / 64 + 1] = 0;
+    dq_init(dq);
     const uint64_t *r0 = rec + boff + e.x;
     uint32_t pl[IPT], dd[IPT], rv[IPT];
 #pragma unroll
@@ -570,7 +765,7 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
         }
     }
     __syncthreads();
-    finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp);
+    finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -617,15 +812,21 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
     const uint32_t b = s.w, n = a.boffs[b + 1] - a.boffs[b];
     const uint32_t nd = s.z + 8;
     const bool final_depth = (uint64_t)nd >= 8ull * n;
+    __shared__ DeferQueue<256> dq;
+    dq_init(dq);
+    __syncthreads();
     auto route = [&](uint32_t gs, uint32_t len) {
         if (len == 1) return;  // resolved by the scatter
         if (final_depth || nd >= kDataMaxBits) {
-            a.groups[atomicAdd(&a.cnt->dgroups, 1u)] = make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u));
-            if (!final_depth) a.bflag[b] = 1;
+            if (!final_depth) {
+                a.bflag[b] = 1;
+                a.cnt->flagged = 1;
+            }
+            dq_push_list(a, dq, make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u)), kListGroups);
         } else if (len <= kBigCap) {
-            push_fin(a, make_uint4(gs, len, nd, b));
+            dq_push(a, dq, gs, len, nd, b, n);
         } else {
-            a.big_next[atomicAdd(&a.cnt->big_next, 1u)] = make_uint4(gs, len, nd, b);
+            dq_push_list(a, dq, make_uint4(gs, len, nd, b), kListBig);
         }
     };
     if (nz == 1) {
@@ -635,6 +836,7 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
         if (d == 0) nomove[blockIdx.x] = 0;
         if (tot > 0) route(s.x + base, tot);
     }
+    dq_flush<256>(a, dq);
 }
 
 __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
@@ -1219,15 +1421,15 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list
     // finish lists by size class; every entry covers > kTinyFin / > kFinCap positions
-    Seg4 *fint_cur = (Seg4 *)c->get(WS_FINT_CUR, seg_cap * 16);
-    Seg4 *fint_nxt = (Seg4 *)c->get(WS_FINT_NXT, seg_cap * 16);
-    Seg4 *fin_cur = (Seg4 *)c->get(WS_FIN_CUR, (N / (kTinyFin + 1) + 2) * 16);
-    Seg4 *fin_nxt = (Seg4 *)c->get(WS_FIN_NXT, (N / (kTinyFin + 1) + 2) * 16);
-    Seg4 *finb_cur = (Seg4 *)c->get(WS_FINB_CUR, (N / (kFinCap + 1) + 2) * 16);
-    Seg4 *finb_nxt = (Seg4 *)c->get(WS_FINB_NXT, (N / (kFinCap + 1) + 2) * 16);
+    Seg4 *const fint_a = (Seg4 *)c->get(WS_FINT_CUR, seg_cap * 16);
+    Seg4 *const fint_b = (Seg4 *)c->get(WS_FINT_NXT, seg_cap * 16);
+    Seg4 *const fin_a = (Seg4 *)c->get(WS_FIN_CUR, (N / (kTinyFin + 1) + 2) * 16);
+    Seg4 *const fin_b = (Seg4 *)c->get(WS_FIN_NXT, (N / (kTinyFin + 1) + 2) * 16);
+    Seg4 *const finb_a = (Seg4 *)c->get(WS_FINB_CUR, (N / (kFinCap + 1) + 2) * 16);
+    Seg4 *const finb_b = (Seg4 *)c->get(WS_FINB_NXT, (N / (kFinCap + 1) + 2) * 16);
     Seg4 *dgroups = (Seg4 *)c->get(WS_GROUPS, seg_cap * 16);
-    Seg4 *big = (Seg4 *)c->get(WS_LARGE, (N / kFinCap + 2) * 16);
-    Seg4 *big2 = (Seg4 *)c->get(WS_LARGE2, (N / kFinCap + 2) * 16);
+    Seg4 *const big = (Seg4 *)c->get(WS_LARGE, (N / kFinCap + 2) * 16);
+    Seg4 *const big2 = (Seg4 *)c->get(WS_LARGE2, (N / kFinCap + 2) * 16);
     uint32_t *bflag = (uint32_t *)c->get(WS_OFFS, nb * 4 + 64);
     uint32_t *d_prim = (uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);
     Counters *d_cnt = (Counters *)c->get(WS_COUNTERS, sizeof(Counters) + 64);
@@ -1248,71 +1450,108 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     da.groups = dgroups;
     da.cnt = d_cnt;
 
-    BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
-    BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
-    BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
+    // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
+    // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
+    // with every SA entry stored, and the context keeps that mode while its batches need it.
+    bool full_sa = c->bwt_full_sa;
+    for (;;) {
+        da.full_sa = full_sa ? 1u : 0u;
+        Seg4 *fint_cur = fint_a, *fint_nxt = fint_b, *fin_cur = fin_a, *fin_nxt = fin_b;
+        Seg4 *finb_cur = finb_a, *finb_nxt = finb_b;
+        BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
+        BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
+        BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
 
-    // ---- data phase
-    BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-    BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, finb_cur, big,
-               d_cnt);
-    BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
-    // the dense finish appends deferred segments after the global pass's list entries
-    da.fin_next = fin_cur;
-    da.fint_next = fint_cur;
-    da.finb_next = finb_cur;
-    da.big_next = big2;
-    BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
-               da, bk, rec);
-    read_counters();
-    uint32_t nfin = h_cnt->fin_next, nfint = h_cnt->fint_next, nfinb = h_cnt->finb_next, nbig = h_cnt->big;
-    Seg4 *big_cur = big, *big_nxt = big2;
-    std::vector<Seg4> hs;
-    std::vector<DTile> ht;
-    std::vector<uint2> hst;
-    while (nfin > 0 || nfint > 0 || nfinb > 0 || nbig > 0) {
-        BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 16, c->stream));  // fin_next, fint_next, finb_next, big_next
-        // every pass of a round writes the other buffer of each list
-        da.fin_next = fin_nxt;
-        da.fint_next = fint_nxt;
-        da.finb_next = finb_nxt;
-        da.big_next = big_nxt;
-        if (nfint > 0) BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4), 256, 0, da, fint_cur, nfint);
-        if (nfin > 0) BMH_LAUNCH(c, "bwt_finish", (k_finish_seg<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
-        if (nfinb > 0)
-            BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfinb, kBigNT, 0, da, finb_cur, kFinCap);
-        if (nbig > 0) {
-            hs.resize(nbig);
-            c->d2h(hs.data(), big_cur, nbig * sizeof(Seg4));
-            c->sync();
-            build_tiles<Seg4, DTile>(hs, kDTile, ht, hst, [](const Seg4 &s) { return s.x; },
-                                     [](const Seg4 &s) { return s.y; });
-            const uint32_t ntl = (uint32_t)ht.size();
-            uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(DTile) + nbig * 8 + nbig * 4 + 64);
-            DTile *d_tiles = (DTile *)d_lt;
-            uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(DTile));
-            uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(DTile) + nbig * 8);
-            c->h2d(d_tiles, ht.data(), ntl * sizeof(DTile));
-            c->h2d(d_segtiles, hst.data(), nbig * 8);
-            uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
-            uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
-            da.fin_next = fin_nxt;
-            da.big_next = big_nxt;
-            BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, thist);
-            BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, thist, stot, d_nomove);
-            BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, d_nomove, thist, stot, sa2);
-            BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
-        }
+        // ---- data phase
+        BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
+        BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, finb_cur, big,
+                   d_cnt);
+        BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
+        // the dense finish appends deferred segments after the global pass's list entries
+        da.fin_next = fin_cur;
+        da.fint_next = fint_cur;
+        da.finb_next = finb_cur;
+        da.big_next = big2;
+        BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
+                   da, bk, rec);
         read_counters();
-        nfin = h_cnt->fin_next;
-        nfint = h_cnt->fint_next;
-        nfinb = h_cnt->finb_next;
-        nbig = h_cnt->big_next;
-        std::swap(fin_cur, fin_nxt);
-        std::swap(fint_cur, fint_nxt);
-        std::swap(finb_cur, finb_nxt);
-        std::swap(big_cur, big_nxt);
+        uint32_t nfin = h_cnt->fin_next, nfint = h_cnt->fint_next, nfinb = h_cnt->finb_next, nbig = h_cnt->big;
+        Seg4 *big_cur = big, *big_nxt = big2;
+        std::vector<Seg4> hs;
+        std::vector<DTile> ht;
+        std::vector<uint2> hst;
+        static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
+        int round = 0;
+        while (nfin > 0 || nfint > 0 || nfinb > 0 || nbig > 0) {
+            if (dbg_lists) {  // per-round list census (diagnostics only)
+                auto census = [&](const char *name, const Seg4 *d, uint32_t cnt) {
+                    std::vector<Seg4> h(cnt);
+                    c->d2h(h.data(), d, cnt * sizeof(Seg4));
+                    c->sync();
+                    uint64_t tot = 0, mx = 0, dmin = ~0ull, dmax = 0;
+                    for (auto &e : h) {
+                        tot += e.y;
+                        mx = std::max<uint64_t>(mx, e.y);
+                        dmin = std::min<uint64_t>(dmin, e.z);
+                        dmax = std::max<uint64_t>(dmax, e.z);
+                    }
+                    fprintf(stderr, "round %d %-5s segs %u elems %llu max %llu depth %llu..%llu\n", round, name, cnt,
+                            (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)(cnt ? dmin : 0),
+                            (unsigned long long)dmax);
+                };
+                census("tiny", fint_cur, nfint);
+                census("fin", fin_cur, nfin);
+                census("finb", finb_cur, nfinb);
+                census("big", big_cur, nbig);
+            }
+            ++round;
+            BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 16, c->stream));  // fin_next, fint_next, finb_next, big_next
+            // every pass of a round writes the other buffer of each list
+            da.fin_next = fin_nxt;
+            da.fint_next = fint_nxt;
+            da.finb_next = finb_nxt;
+            da.big_next = big_nxt;
+            if (nfint > 0)
+                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4 * kTinyPerWave), 256, 0, da, fint_cur, nfint);
+            if (nfin > 0) BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
+            if (nfinb > 0)
+                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfinb, kBigNT, 0, da, finb_cur, kFinCap);
+            if (nbig > 0) {
+                hs.resize(nbig);
+                c->d2h(hs.data(), big_cur, nbig * sizeof(Seg4));
+                c->sync();
+                build_tiles<Seg4, DTile>(hs, kDTile, ht, hst, [](const Seg4 &s) { return s.x; },
+                                         [](const Seg4 &s) { return s.y; });
+                const uint32_t ntl = (uint32_t)ht.size();
+                uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(DTile) + nbig * 8 + nbig * 4 + 64);
+                DTile *d_tiles = (DTile *)d_lt;
+                uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(DTile));
+                uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(DTile) + nbig * 8);
+                c->h2d(d_tiles, ht.data(), ntl * sizeof(DTile));
+                c->h2d(d_segtiles, hst.data(), nbig * 8);
+                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
+                uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
+                da.fin_next = fin_nxt;
+                da.big_next = big_nxt;
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, thist);
+                BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, thist, stot, d_nomove);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, d_nomove, thist, stot, sa2);
+                BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
+            }
+            read_counters();
+            nfin = h_cnt->fin_next;
+            nfint = h_cnt->fint_next;
+            nfinb = h_cnt->finb_next;
+            nbig = h_cnt->big_next;
+            std::swap(fin_cur, fin_nxt);
+            std::swap(fint_cur, fint_nxt);
+            std::swap(finb_cur, finb_nxt);
+            std::swap(big_cur, big_nxt);
+        }
+        if (full_sa || h_cnt->flagged == 0) break;
+        full_sa = true;
     }
+    c->bwt_full_sa = h_cnt->flagged != 0;
 
     // ---- doubling phase, only if some block still holds tied groups
     wall_data.stop();
