@@ -44,7 +44,7 @@ constexpr uint32_t kFinNT = 256, kFinCap = 4096;
 constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
-constexpr uint32_t kDataMaxBits = 64;           // deeper MSD ties go to rank doubling
+constexpr uint32_t kDataMaxBits = 512;          // deeper MSD ties go to rank doubling
 constexpr uint32_t kFinMaxBits = 512;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
 constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries per workgroup
@@ -202,7 +202,7 @@ __device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q
         q.e[i] = sg;
         q.tag[i] = (l << 24) | atomicAdd(&q.cnt[l], 1u);
     } else {
-        list_base(a, l)[atomicAdd(list_counter(a, l), 1u)] = sg;
+        list_base(a, l)[wave_append(list_counter(a, l))] = sg;
     }
 }
 
@@ -317,9 +317,9 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     for (uint32_t k = 0; k < nc; ++k) chist[(size_t)(c0 + 8 * k) * kG1Bins + d] += start;
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
     if (run > kBigCap)
-        big[atomicAdd(&cnt->big, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        big[wave_append(&cnt->big)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[atomicAdd(&cnt->finb_next, 1u)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        fin[wave_append(&cnt->finb_next)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -614,19 +614,45 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     const uint32_t t = threadIdx.x;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     if (t == 0) s_tmp[NT / 64 + 1] = 0;
+    __shared__ uint32_t s_or[2];
+    if (t < 2) s_or[t] = 0;
+    // skip the bits every rotation of the segment shares (on text, runs inside words): the
+    // counting sort starts at the first bit where two of them differ
+    const uint64_t w0 = rot_window(blk, n, a.sa[gstart], db);
     uint32_t pl[IPT], dd[IPT], rv[IPT];
+    uint64_t wk[IPT], acc = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        wk[k] = 0;
+        if (t + k * NT < len) {
+            pl[k] = a.sa[gstart + t + k * NT];
+            wk[k] = rot_window(blk, n, pl[k], db);
+            acc |= wk[k] ^ w0;
+        }
+    }
+    __syncthreads();
+    if (acc) {
+        atomicOr(&s_or[0], (uint32_t)acc);
+        atomicOr(&s_or[1], (uint32_t)(acc >> 32));
+    }
+    __syncthreads();
+    const uint64_t orv = ((uint64_t)s_or[1] << 32) | s_or[0];
+    if (orv == 0) {  // equal in all 64 bits: the whole segment goes on, 64 bits deeper
+        if (t == 0) dq_push(a, dq, gstart, len, (uint32_t)min<uint64_t>((uint64_t)db + 64, 0xffffffffull), b, n);
+        dq_flush<NT>(a, dq);
+        return;
+    }
+    const uint32_t cp = (uint32_t)__builtin_clzll(orv);
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         if (t + k * NT < len) {
-            const uint32_t p = a.sa[gstart + t + k * NT];
-            const uint64_t w = rot_window(blk, n, p, db);
-            pl[k] = p;
+            // the next 44 bits after the shared prefix: from the window, or gathered again
+            const uint64_t w = cp <= 20 ? wk[k] << cp : rot_window(blk, n, pl[k], db + cp);
             dd[k] = (uint32_t)(w >> (64 - kSegDigit));
             rv[k] = (uint32_t)(w >> (32 - kSegDigit));
         }
     }
-    __syncthreads();
-    finish_core<NT, CAP>(a, gstart, len, db, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+    finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
 constexpr uint32_t kSortQ = 1024;  // deferral queue of k_finish_sort (overlays its key array)
@@ -773,26 +799,61 @@ struct DTile {
     uint32_t seg, start, len, pad;
 };
 
+// Bits every rotation of an MSD segment shares below its depth (OR of window XORs against
+// the segment's first rotation); the digit of the pass is taken right after them.
+__global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                             unsigned long long *__restrict__ segor)
+{
+    __shared__ uint32_t s_or[2];
+    const DTile t = tiles[blockIdx.x];
+    const Seg4 s = segs[t.seg];
+    const uint32_t boff = a.boffs[s.w], n = a.boffs[s.w + 1] - boff;
+    const uint8_t *blk = a.data + boff;
+    if (threadIdx.x < 2) s_or[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t w0 = rot_window(blk, n, a.sa[s.x], s.z);
+    uint64_t acc = 0;
+    for (uint32_t e = threadIdx.x; e < t.len; e += 256) acc |= rot_window(blk, n, a.sa[t.start + e], s.z) ^ w0;
+    if (acc) {
+        atomicOr(&s_or[0], (uint32_t)acc);
+        atomicOr(&s_or[1], (uint32_t)(acc >> 32));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && (s_or[0] | s_or[1])) atomicOr(&segor[t.seg], ((unsigned long long)s_or[1] << 32) | s_or[0]);
+}
+
+// depth of the pass digit: the segment depth plus its shared bits (64: no digit in the window)
+__device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint32_t seg)
+{
+    const unsigned long long o = segor[seg];
+    return o ? (uint32_t)__builtin_clzll(o) : 64u;
+}
+
 __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                               uint32_t *__restrict__ thist)
+                                               const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist)
 {
     __shared__ uint32_t h[256];
     const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
     const uint32_t boff = a.boffs[s.w], n = a.boffs[s.w + 1] - boff;
     const uint8_t *blk = a.data + boff;
+    const uint32_t cp = seg_cp(segor, t.seg);
     h[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256)
-        atomicAdd(&h[(uint32_t)(rot_window(blk, n, a.sa[t.start + e], s.z) >> 56)], 1u);
+    if (cp == 64) {
+        if (threadIdx.x == 0) h[0] = t.len;
+    } else {
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256)
+            atomicAdd(&h[(uint32_t)(rot_window(blk, n, a.sa[t.start + e], s.z + cp) >> 56)], 1u);
+    }
     __syncthreads();
     thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
 // grid = nsegs; 256 threads (digits). Offsets in place; sub-segment routing.
 __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint2 *__restrict__ segtiles,
-                                               uint32_t *__restrict__ thist, uint32_t *__restrict__ stot,
-                                               uint32_t *__restrict__ nomove)
+                                               const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
+                                               uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove)
 {
     __shared__ uint32_t s_tmp[8];
     const Seg4 s = segs[blockIdx.x];
@@ -810,7 +871,8 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
     stot[(size_t)blockIdx.x * 256 + d] = tot;
     const uint32_t b = s.w, n = a.boffs[b + 1] - a.boffs[b];
-    const uint32_t nd = s.z + 8;
+    const uint32_t cp = seg_cp(segor, blockIdx.x);
+    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)s.z + (cp == 64 ? 64u : cp + 8u), 0xffffffffull);
     const bool final_depth = (uint64_t)nd >= 8ull * n;
     __shared__ DeferQueue<256> dq;
     dq_init(dq);
@@ -840,6 +902,7 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
 }
 
 __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                                  const unsigned long long *__restrict__ segor,
                                                   const uint32_t *__restrict__ nomove, const uint32_t *__restrict__ thist,
                                                   const uint32_t *__restrict__ stot, uint32_t *__restrict__ sa2)
 {
@@ -849,12 +912,13 @@ __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__rest
     const uint32_t b = s.w, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     if (nomove[t.seg]) return;  // one digit only: nothing moves
+    const uint32_t cp = seg_cp(segor, t.seg);
     cur[threadIdx.x] = thist[(size_t)blockIdx.x * 256 + threadIdx.x];
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
         const uint32_t j = t.start + e;
         const uint32_t p = a.sa[j];
-        const uint32_t d = (uint32_t)(rot_window(blk, n, p, s.z) >> 56);
+        const uint32_t d = (uint32_t)(rot_window(blk, n, p, s.z + cp) >> 56);
         const uint32_t slot = atomicAdd(&cur[d], 1u);
         sa2[slot] = p;
         if (stot[(size_t)t.seg * 256 + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
@@ -914,7 +978,7 @@ __global__ __launch_bounds__(256) void k_group_fill(DataArgs a, const Seg4 *__re
             if (fin) put_final(a, b, boff, n, blk, s.x + e, p, s.x - boff);
         }
         if (!fin && l == 0) {
-            segs[atomicAdd(&cnt->next, 1u)] = make_uint2(s.x, s.y);
+            segs[wave_append(&cnt->next)] = make_uint2(s.x, s.y);
             atomicMin(&cnt->dmin_bits, s.z);
         }
     }
@@ -952,7 +1016,7 @@ __device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32
     const bool final_ = gsz == 1 || a.newD >= n;
     a.rk_nxt[boff + p] = gs;
     if (final_) {
-        const uint32_t i = atomicAdd(&a.cnt->resolved, 1u);
+        const uint32_t i = wave_append(&a.cnt->resolved);
         a.resolved[i] = boff + p;
         a.L[gslot] = a.data[boff + (p == 0 ? n - 1 : p - 1)];
         if (p == 0) {
@@ -960,7 +1024,7 @@ __device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32
             a.prim[b] = gs;
         }
     } else if (first) {
-        const uint32_t i = atomicAdd(&a.cnt->next, 1u);
+        const uint32_t i = wave_append(&a.cnt->next);
         a.next[i] = make_uint2(boff + gs, gsz);
     }
 }
@@ -972,16 +1036,16 @@ __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 
     if (i >= nseg) return;
     const uint2 s = segs[i];
     if (s.y <= kTinyMax) {
-        tiny[atomicAdd(&cnt->tiny, 1u)] = s;
+        tiny[wave_append(&cnt->tiny)] = s;
     } else if (s.y <= kMedMax) {
-        med[atomicAdd(&cnt->med, 1u)] = s;
+        med[wave_append(&cnt->med)] = s;
     } else {
         LSeg l;
         l.gstart = s.x;
         l.len = s.y;
         l.shift = 24;
         l.gathered = 0;
-        large[atomicAdd(&cnt->large, 1u)] = l;
+        large[wave_append(&cnt->large)] = l;
     }
 }
 
@@ -1038,7 +1102,7 @@ __global__ void k_tile_heads(const uint32_t *__restrict__ prefix, uint32_t n, ui
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t t = prefix[i] / kTileT;
-    if (i == 0 || prefix[i - 1] / kTileT != t) tiles[atomicAdd(&cnt->tiles, 1u)] = i;
+    if (i == 0 || prefix[i - 1] / kTileT != t) tiles[wave_append(&cnt->tiles)] = i;
 }
 
 // One workgroup per tile of consecutive tiny segments (<= 1152 elements). Each element's new
@@ -1228,20 +1292,20 @@ __device__ __forceinline__ void push_sub(uint32_t gstart, uint32_t len, uint32_t
                                          LSeg *large_next, uint2 *groups, Counters *cnt)
 {
     if (len == 1) {
-        groups[atomicAdd(&cnt->groups, 1u)] = make_uint2(gstart, len);
+        groups[wave_append(&cnt->groups)] = make_uint2(gstart, len);
     } else if (len <= kTinyMax) {
-        tiny[atomicAdd(&cnt->tiny, 1u)] = make_uint2(gstart, len);
+        tiny[wave_append(&cnt->tiny)] = make_uint2(gstart, len);
     } else if (len <= kMedMax) {
-        med[atomicAdd(&cnt->med, 1u)] = make_uint2(gstart, len);
+        med[wave_append(&cnt->med)] = make_uint2(gstart, len);
     } else if (shift > 0) {
         LSeg l;
         l.gstart = gstart;
         l.len = len;
         l.shift = shift - 8;
         l.gathered = 1;
-        large_next[atomicAdd(&cnt->large_next, 1u)] = l;
+        large_next[wave_append(&cnt->large_next)] = l;
     } else {
-        groups[atomicAdd(&cnt->groups, 1u)] = make_uint2(gstart, len);  // keys exhausted: equal
+        groups[wave_append(&cnt->groups)] = make_uint2(gstart, len);  // keys exhausted: equal
     }
 }
 
@@ -1533,9 +1597,13 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
                 da.fin_next = fin_nxt;
                 da.big_next = big_nxt;
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, thist);
-                BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, thist, stot, d_nomove);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, d_nomove, thist, stot, sa2);
+                unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 8 + 64);
+                BMH_HIP(hipMemsetAsync(segor, 0, (size_t)nbig * 8, c->stream));
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, thist);
+                BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, segor, thist, stot, d_nomove);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, d_nomove, thist, stot,
+                           sa2);
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
             }
             read_counters();

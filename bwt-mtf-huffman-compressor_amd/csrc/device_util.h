@@ -16,6 +16,20 @@ __device__ __forceinline__ uint32_t writelane(uint32_t val, uint32_t lane, uint3
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// One slot of a global list for every active lane, with ONE atomic per wave: callers in
+// divergent code get consecutive indices (single-lane atomics on a shared counter serialise
+// at the L2 when thousands of waves append).
+__device__ __forceinline__ uint32_t wave_append(uint32_t *ctr)
+{
+    const uint64_t act = __ballot(1);
+    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__builtin_popcountll(act));
+    base = (uint32_t)__shfl((int)base, (int)leader, 64);
+    return base + rank;
+}
+
 // Inclusive wave64 scans.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
 {
