@@ -58,7 +58,8 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t fin_next, fint_next, finb_next, big_next, big, dgroups, dmin_bits, flagged;  // data phase
+    uint32_t lcnt[5];  // data phase: entries of each list (kListTiny .. kListGroups)
+    uint32_t big, dmin_bits, flagged;
 };
 
 // Data-phase segment / group: {gstart (batch slot), len, bit depth, block (| kFinalFlag)}
@@ -83,11 +84,7 @@ struct DataArgs {
     uint8_t *L;
     uint32_t *prim;
     uint32_t *bflag;   // block keeps tied groups -> needs the rank phase
-    Seg4 *groups;      // tied groups (unresolved or final)
-    Seg4 *fin_next;    // deferred finish segments, 64 < len <= kFinCap
-    Seg4 *fint_next;   // deferred finish segments, len <= kTinyFin
-    Seg4 *finb_next;   // deferred finish segments, len > kFinCap
-    Seg4 *big_next;    // MSD segments for the next pass
+    Seg4 *const *lists;  // device table: the list each deferral class appends to (kList*)
     Counters *cnt;
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
 };
@@ -134,29 +131,11 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
 }
 
 // The lists a deferred segment can go to.
-enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListGroups = 3, kListBig = 4, kNumLists = 5 };
+// The first four are refilled every round; the groups list grows over the whole data phase.
+enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListBig = 3, kListGroups = 4, kNumLists = 5 };
 
-__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l)
-{
-    switch (l) {
-    case kListTiny: return &a.cnt->fint_next;
-    case kListFin: return &a.cnt->fin_next;
-    case kListFinb: return &a.cnt->finb_next;
-    case kListGroups: return &a.cnt->dgroups;
-    default: return &a.cnt->big_next;
-    }
-}
-
-__device__ __forceinline__ Seg4 *list_base(const DataArgs &a, uint32_t l)
-{
-    switch (l) {
-    case kListTiny: return a.fint_next;
-    case kListFin: return a.fin_next;
-    case kListFinb: return a.finb_next;
-    case kListGroups: return a.groups;
-    default: return a.big_next;
-    }
-}
+__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l) { return &a.cnt->lcnt[l]; }
+__device__ __forceinline__ Seg4 *list_base(const DataArgs &a, uint32_t l) { return a.lists[l]; }
 
 // A tied run of m rotations, grouped up to bit depth nd (sg = {gs, m, nd, b}): another finish
 // pass by size class, or rank doubling once it is deep (long repeats), or final when nd
@@ -215,15 +194,17 @@ __device__ __forceinline__ void dq_push(const DataArgs &a, DeferQueue<Q> &q, uin
     dq_push_list(a, q, sg, l);
 }
 
-// all threads, once per queue; starts and ends with a barrier
+// all threads, once per queue; starts with a barrier, and ends with one when anything was
+// queued (the common empty case costs the one barrier)
 template <uint32_t NT, uint32_t Q>
 __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
 {
     __syncthreads();
+    const uint32_t qn = min(q.n, Q);
+    if (qn == 0) return;  // workgroup-uniform
     const uint32_t t = threadIdx.x;
     if (t < kNumLists && q.cnt[t]) q.base[t] = atomicAdd(list_counter(a, t), q.cnt[t]);
     __syncthreads();
-    const uint32_t qn = min(q.n, Q);
     for (uint32_t i = t; i < qn; i += NT) {
         const uint32_t tg = q.tag[i], l = tg >> 24;
         list_base(a, l)[q.base[l] + (tg & 0xffffffu)] = q.e[i];
@@ -319,7 +300,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     if (run > kBigCap)
         big[wave_append(&cnt->big)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[wave_append(&cnt->finb_next)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        fin[wave_append(&cnt->lcnt[kListFinb])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -620,14 +601,15 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     // counting sort starts at the first bit where two of them differ
     const uint64_t w0 = rot_window(blk, n, a.sa[gstart], db);
     uint32_t pl[IPT], dd[IPT], rv[IPT];
-    uint64_t wk[IPT], acc = 0;
+    uint64_t acc = 0;
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
-        wk[k] = 0;
         if (t + k * NT < len) {
             pl[k] = a.sa[gstart + t + k * NT];
-            wk[k] = rot_window(blk, n, pl[k], db);
-            acc |= wk[k] ^ w0;
+            const uint64_t w = rot_window(blk, n, pl[k], db);
+            acc |= w ^ w0;
+            dd[k] = (uint32_t)(w >> (64 - kSegDigit));
+            rv[k] = (uint32_t)(w >> (32 - kSegDigit));
         }
     }
     __syncthreads();
@@ -643,13 +625,14 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
         return;
     }
     const uint32_t cp = (uint32_t)__builtin_clzll(orv);
+    if (cp) {  // the 44 bits after the shared prefix, gathered again
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        if (t + k * NT < len) {
-            // the next 44 bits after the shared prefix: from the window, or gathered again
-            const uint64_t w = cp <= 20 ? wk[k] << cp : rot_window(blk, n, pl[k], db + cp);
-            dd[k] = (uint32_t)(w >> (64 - kSegDigit));
-            rv[k] = (uint32_t)(w >> (32 - kSegDigit));
+        for (uint32_t k = 0; k < IPT; ++k) {
+            if (t + k * NT < len) {
+                const uint64_t w = rot_window(blk, n, pl[k], db + cp);
+                dd[k] = (uint32_t)(w >> (64 - kSegDigit));
+                rv[k] = (uint32_t)(w >> (32 - kSegDigit));
+            }
         }
     }
     finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
@@ -1511,8 +1494,21 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     da.L = d_L;
     da.prim = d_prim;
     da.bflag = bflag;
-    da.groups = dgroups;
     da.cnt = d_cnt;
+    Seg4 **d_lists = (Seg4 **)c->get(WS_LISTS, kNumLists * sizeof(Seg4 *) + 64);
+    // the lists the next pass appends to: a device table uploaded in stream order (kernels
+    // queued before the upload have read the previous one)
+    auto set_lists = [&](Seg4 *tiny, Seg4 *fin, Seg4 *finb, Seg4 *bigl) {
+        Seg4 *h[kNumLists];
+        h[kListTiny] = tiny;
+        h[kListFin] = fin;
+        h[kListFinb] = finb;
+        h[kListBig] = bigl;
+        h[kListGroups] = dgroups;
+        c->h2d(d_lists, h, sizeof(h));
+        Seg4 **d = d_lists;
+        da.lists = d;
+    };
 
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
@@ -1532,14 +1528,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                    d_cnt);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
-        da.fin_next = fin_cur;
-        da.fint_next = fint_cur;
-        da.finb_next = finb_cur;
-        da.big_next = big2;
+        set_lists(fint_cur, fin_cur, finb_cur, big2);
         BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
                    da, bk, rec);
         read_counters();
-        uint32_t nfin = h_cnt->fin_next, nfint = h_cnt->fint_next, nfinb = h_cnt->finb_next, nbig = h_cnt->big;
+        uint32_t nfin = h_cnt->lcnt[kListFin], nfint = h_cnt->lcnt[kListTiny], nfinb = h_cnt->lcnt[kListFinb];
+        uint32_t nbig = h_cnt->big;
         Seg4 *big_cur = big, *big_nxt = big2;
         std::vector<Seg4> hs;
         std::vector<DTile> ht;
@@ -1569,12 +1563,9 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 census("big", big_cur, nbig);
             }
             ++round;
-            BMH_HIP(hipMemsetAsync(&d_cnt->fin_next, 0, 16, c->stream));  // fin_next, fint_next, finb_next, big_next
+            BMH_HIP(hipMemsetAsync(&d_cnt->lcnt[0], 0, 16, c->stream));  // the four per-round lists
             // every pass of a round writes the other buffer of each list
-            da.fin_next = fin_nxt;
-            da.fint_next = fint_nxt;
-            da.finb_next = finb_nxt;
-            da.big_next = big_nxt;
+            set_lists(fint_nxt, fin_nxt, finb_nxt, big_nxt);
             if (nfint > 0)
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4 * kTinyPerWave), 256, 0, da, fint_cur, nfint);
             if (nfin > 0) BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
@@ -1595,8 +1586,6 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 c->h2d(d_segtiles, hst.data(), nbig * 8);
                 uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
                 uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
-                da.fin_next = fin_nxt;
-                da.big_next = big_nxt;
                 unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 8 + 64);
                 BMH_HIP(hipMemsetAsync(segor, 0, (size_t)nbig * 8, c->stream));
                 BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor);
@@ -1607,10 +1596,10 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
             }
             read_counters();
-            nfin = h_cnt->fin_next;
-            nfint = h_cnt->fint_next;
-            nfinb = h_cnt->finb_next;
-            nbig = h_cnt->big_next;
+            nfin = h_cnt->lcnt[kListFin];
+            nfint = h_cnt->lcnt[kListTiny];
+            nfinb = h_cnt->lcnt[kListFinb];
+            nbig = h_cnt->lcnt[kListBig];
             std::swap(fin_cur, fin_nxt);
             std::swap(fint_cur, fint_nxt);
             std::swap(finb_cur, finb_nxt);
@@ -1624,7 +1613,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // ---- doubling phase, only if some block still holds tied groups
     wall_data.stop();
     WallPhase wall_dbl(c, "bwt_doubling");
-    const uint32_t ngroups = h_cnt->dgroups;
+    const uint32_t ngroups = h_cnt->lcnt[kListGroups];
     if (ngroups > 0) {
         uint32_t *rkA = (uint32_t *)c->get(WS_RKA, N * 4);
         uint32_t *rkB = (uint32_t *)c->get(WS_RKB, N * 4);

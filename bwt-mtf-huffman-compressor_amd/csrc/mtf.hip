@@ -292,18 +292,20 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
                 o[k >> 2] |= (ix[j] & 255u) << (8 * (k & 3));
             }
             now += kMtfGroup;
-            if (now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
-                for (uint32_t s0 = 0; s0 < 256; s0 += 16) {  // 16 independent reads in flight
-                    uint32_t ts[16];
+        }
+        // a group of 16 symbols advances `now` by 16 from 256, so the window fills up
+        // exactly at a group boundary
+        if (now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
+            for (uint32_t s0 = 0; s0 < 256; s0 += 16) {  // 16 independent reads in flight
+                uint32_t ts[16];
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) ts[k] = tm[(s0 + k) * kLanes + l];
+                for (int k = 0; k < 16; ++k) ts[k] = tm[(s0 + k) * kLanes + l];
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) ts[k] = 255 - marks_above(ts[k], S, bits, cnt, l);
+                for (int k = 0; k < 16; ++k) ts[k] = 255 - marks_above(ts[k], S, bits, cnt, l);
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) tm[(s0 + k) * kLanes + l] = (uint16_t)ts[k];
-                }
-                window_reset(bits, cnt, l, S, now);
+                for (int k = 0; k < 16; ++k) tm[(s0 + k) * kLanes + l] = (uint16_t)ts[k];
             }
+            window_reset(bits, cnt, l, S, now);
         }
         if (full) {
             *(uint4 *)(out + a) = o4;
