@@ -17,8 +17,9 @@
 //                words above inside c's superword (byte counters in LDS), bits above inside
 //                c's word (one popcount). An access clears one mark and sets the next slot —
 //                O(1) work instead of moving up to 255 list entries; the window is renumbered
-//                every 256 symbols. (tools/microbench/mtf_variants.hip: 4.6 ms per GiB vs
-//                28-40 ms for whole-wave list updates on MI355X.)
+//                every 256 symbols. Stamps are stored as a byte + an "accessed this epoch" bit
+//                (288 B per lane), one-wave workgroups. (tools/microbench/mtf_variants.hip:
+//                4.6 ms per GiB vs 28-40 ms for whole-wave list updates on MI355X.)
 //   4. hist    : freq + first occurrence of each MTF value per block (LDS atomics).
 #include "bmh_internal.h"
 #include "device_util.h"
@@ -30,7 +31,7 @@ namespace bmh {
 namespace {
 
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
-constexpr int kLanes = 128;           // lanes (chunks) per encode workgroup
+constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
 constexpr int kMtfGroup = 2;          // symbols per batched MTF step
 
 struct MChunk {
@@ -138,6 +139,27 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__
     }
 }
 
+// Time stamps are 9-bit slots kept as a byte (tm8, the low 8 bits) plus an epoch bit (ep: the
+// symbol was accessed since the last renumbering, i.e. its slot is >= 256): 288 B of LDS per
+// lane instead of 512, so six one-wave workgroups fit a CU instead of four waves. A lane's
+// bytes for symbols 4k..4k+3 share one dword, and dword k of lane l sits at k * kLanes + l
+// (every lane in its own bank).
+__device__ __forceinline__ uint32_t tm8_index(uint32_t c, uint32_t l) { return ((c >> 2) * kLanes + l) * 4 + (c & 3u); }
+
+__device__ __forceinline__ uint32_t stamp_read(const uint8_t *tm8, const uint32_t *ep, uint32_t c, uint32_t l)
+{
+    const uint32_t lo = tm8[tm8_index(c, l)];
+    const uint32_t e = ep[(c >> 5) * kLanes + l];
+    return lo | (((e >> (c & 31u)) & 1u) << 8);
+}
+
+// a new slot (>= 256) for symbol c
+__device__ __forceinline__ void stamp_write_new(uint8_t *tm8, uint32_t *ep, uint32_t c, uint32_t l, uint32_t slot)
+{
+    tm8[tm8_index(c, l)] = (uint8_t)slot;
+    atomicOr(&ep[(c >> 5) * kLanes + l], 1u << (c & 31u));
+}
+
 // Marks above slot t: bits above in t's word + words above in t's superword + superwords above.
 __device__ __forceinline__ uint32_t marks_above(uint32_t t, uint32_t S, const uint32_t *bits, const uint32_t *cnt,
                                                 uint32_t l)
@@ -169,13 +191,13 @@ __device__ __forceinline__ void window_reset(uint32_t *bits, uint32_t *cnt, uint
 // Then the state update: each first occurrence clears its old mark, each last occurrence
 // takes slot now0 + j (one OR per group: the G slots share a word).
 template <int G>
-__device__ __forceinline__ uint32_t mtf_group(const uint32_t (&c)[G], uint32_t vmask, uint16_t *tm, uint32_t *bits,
-                                              uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t now0,
+__device__ __forceinline__ uint32_t mtf_group(const uint32_t (&c)[G], uint32_t vmask, uint8_t *tm8, uint32_t *ep,
+                                              uint32_t *bits, uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t now0,
                                               uint32_t (&idx)[G])
 {
     uint32_t t[G], base[G], prev[G];
 #pragma unroll
-    for (int j = 0; j < G; ++j) t[j] = tm[c[j] * kLanes + l];
+    for (int j = 0; j < G; ++j) t[j] = stamp_read(tm8, ep, c[j], l);
 #pragma unroll
     for (int j = 0; j < G; ++j) base[j] = marks_above(t[j], S, bits, cnt, l);
     uint32_t first = 0, lastm = vmask;
@@ -218,7 +240,7 @@ __device__ __forceinline__ uint32_t mtf_group(const uint32_t (&c)[G], uint32_t v
     S += np << (8 * (wn >> 2));
 #pragma unroll
     for (int j = 0; j < G; ++j)
-        if ((lastm >> j) & 1u) tm[c[j] * kLanes + l] = (uint16_t)(now0 + j);
+        if ((lastm >> j) & 1u) stamp_write_new(tm8, ep, c[j], l, now0 + j);
     return 0;
 }
 
@@ -231,8 +253,10 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
                                                        uint32_t nch, const uint32_t *__restrict__ Sst,
                                                        uint8_t *__restrict__ out)
 {
-    __shared__ uint16_t tm[256 * kLanes];
+    __shared__ uint32_t tm32[64 * kLanes];  // the stamp bytes (tm8_index)
+    __shared__ uint32_t ep[8 * kLanes];
     __shared__ uint32_t bits[16 * kLanes];
+    uint8_t *tm8 = (uint8_t *)tm32;
     __shared__ uint32_t cnt[4 * kLanes];
     const uint32_t l = threadIdx.x;
     const uint32_t g = blockIdx.x * kLanes + l;
@@ -242,9 +266,10 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         const uint32_t *st = Sst + (size_t)g * 64;
         for (uint32_t k4 = 0; k4 < 64; ++k4) {
             const uint32_t w = st[k4];
-            for (uint32_t j = 0; j < 4; ++j) tm[((w >> (8 * j)) & 255u) * kLanes + l] = (uint16_t)(255 - (4 * k4 + j));
+            for (uint32_t j = 0; j < 4; ++j) tm8[tm8_index((w >> (8 * j)) & 255u, l)] = (uint8_t)(255 - (4 * k4 + j));
         }
     }
+    for (uint32_t w = 0; w < 8; ++w) ep[w * kLanes + l] = 0;
     uint32_t S, now;
     window_reset(bits, cnt, l, S, now);
     const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
@@ -285,7 +310,8 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
                 const int k = h * kMtfGroup + j;
                 cs[j] = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
             }
-            mtf_group<kMtfGroup>(cs, (vm >> (h * kMtfGroup)) & ((1u << kMtfGroup) - 1), tm, bits, cnt, l, S, now, ix);
+            mtf_group<kMtfGroup>(cs, (vm >> (h * kMtfGroup)) & ((1u << kMtfGroup) - 1), tm8, ep, bits, cnt, l, S, now,
+                                 ix);
 #pragma unroll
             for (int j = 0; j < kMtfGroup; ++j) {
                 const int k = h * kMtfGroup + j;
@@ -296,15 +322,30 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         // a group of 16 symbols advances `now` by 16 from 256, so the window fills up
         // exactly at a group boundary
         if (now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
+            uint32_t e8[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) e8[w] = ep[w * kLanes + l];
             for (uint32_t s0 = 0; s0 < 256; s0 += 16) {  // 16 independent reads in flight
-                uint32_t ts[16];
+                uint32_t tw[4], nw[4];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) ts[k] = tm[(s0 + k) * kLanes + l];
+                for (int k = 0; k < 4; ++k) tw[k] = tm32[((s0 >> 2) + k) * kLanes + l];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) ts[k] = 255 - marks_above(ts[k], S, bits, cnt, l);
+                for (int k = 0; k < 4; ++k) nw[k] = 0;
 #pragma unroll
-                for (int k = 0; k < 16; ++k) tm[(s0 + k) * kLanes + l] = (uint16_t)ts[k];
+                for (int k = 0; k < 16; ++k) {
+                    const uint32_t c = s0 + k;
+                    uint32_t e = 0;
+#pragma unroll
+                    for (int w = 0; w < 8; ++w)  // c >> 5 is uniform per unrolled step
+                        if ((uint32_t)w == (c >> 5)) e = e8[w];
+                    const uint32_t ts = ((tw[k >> 2] >> (8 * (k & 3))) & 255u) | (((e >> (c & 31u)) & 1u) << 8);
+                    nw[k >> 2] |= (255u - marks_above(ts, S, bits, cnt, l)) << (8 * (k & 3));
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) tm32[((s0 >> 2) + k) * kLanes + l] = nw[k];
             }
+#pragma unroll
+            for (int w = 0; w < 8; ++w) ep[w * kLanes + l] = 0;
             window_reset(bits, cnt, l, S, now);
         }
         if (full) {

@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 NAMES = [
-    (r"k_finish_dense", "bwt_finish_dense"), (r"k_finish_seg<256u?, 4096u?>", "bwt_finish"),
+    (r"k_finish_dense", "bwt_finish_dense"), (r"k_finish_sort<256u?, 4096u?>", "bwt_finish"),
     (r"k_finish_seg<1024u?, 19072u?>", "bwt_finish_big"), (r"k_g1_hist", "bwt_g1_hist"),
     (r"k_g1_scan", "bwt_g1_scan"), (r"k_g1_scatter", "bwt_g1_scatter"), (r"k_mtf_recency", "mtf_recency"),
     (r"k_mtf_compose", "mtf_compose"), (r"k_mtf_encode", "mtf_encode"), (r"k_mtf_hist", "mtf_hist"),
