@@ -46,7 +46,7 @@ enum Slot : int {
     WS_LARGE, WS_LARGE2, WS_GROUPS, WS_PREFIX, WS_SCAN_PART, WS_TILES, WS_BLOCKS, WS_OFFS,
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
-    WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
+    WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
     WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_COUNT_
 };
 
@@ -82,6 +82,10 @@ struct Ctx {
     // BWT: write the suffix array of every slot (needed by rank doubling) instead of only the
     // slots later passes read; set after a batch needed doubling, cleared when one did not
     bool bwt_full_sa = false;
+    // host-buffer streaming (capi.cpp): copy streams and two pinned staging slots each way
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    uint8_t *stage_in[2] = {nullptr, nullptr}, *stage_out[2] = {nullptr, nullptr};
+    size_t stage_in_size = 0, stage_out_size = 0;
 
     void *get(Slot s, size_t bytes);
     void *host_pinned(size_t bytes);

@@ -11,6 +11,10 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <thread>
 
 namespace bmh {
@@ -314,68 +318,243 @@ static uint64_t max_batch_bytes()
     return v ? v : (1ull << 30);
 }
 
-// Encode host blocks [b0, b1) of `in` (block size bs); appends records to recs/lens.
-static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t bs, const std::vector<uint64_t> &blist,
-                               std::vector<std::vector<uint8_t>> &recs)
+static uint64_t stream_batch_bytes()
 {
-    const uint64_t cap_batch = max_batch_bytes();
-    size_t i = 0;
-    while (i < blist.size()) {
-        // gather consecutive (in blist order) blocks up to the batch cap
-        std::vector<uint64_t> offs{0};
-        size_t j = i;
-        while (j < blist.size()) {
-            const uint64_t b = blist[j];
-            const uint64_t len = std::min(bs, n - b * bs);
-            if (j > i && offs.back() + len > cap_batch) break;
-            offs.push_back(offs.back() + len);
-            ++j;
+    const char *e = getenv("BMH_STREAM_BATCH");
+    uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    return std::min<uint64_t>(v ? v : (256ull << 20), max_batch_bytes());
+}
+
+// memcpy on up to `nt` threads (pageable <-> pinned staging copies are CPU-bound)
+static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t bytes, unsigned nt)
+{
+    const uint64_t kMin = 8ull << 20;
+    nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nt, bytes / kMin));
+    if (nt <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const uint64_t part = (bytes / nt + 4095) & ~4095ull;
+    for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t o = std::min<uint64_t>(bytes, part * t), e = std::min<uint64_t>(bytes, o + part);
+        if (e > o) th.emplace_back([=] { memcpy(dst + o, src + o, e - o); });
+    }
+    for (auto &x : th) x.join();
+}
+
+static unsigned copy_threads()
+{
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    return std::min(16u, hw);
+}
+
+static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes)
+{
+    if (!c->s_h2d) BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
+    if (!c->s_d2h) BMH_HIP(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
+    if (c->stage_in_size < in_bytes) {
+        for (auto &p : c->stage_in) {
+            if (p) BMH_HIP(hipHostFree(p));
+            p = nullptr;
         }
-        const uint32_t nbk = (uint32_t)(j - i);
-        Batch bt = make_batch(offs.data(), nbk);
-        uint8_t *d_in = (uint8_t *)c->get(WS_IN, bt.total);
-        for (size_t k = i; k < j; ++k) {
-            const uint64_t b = blist[k];
-            BMH_HIP(hipMemcpyAsync(d_in + offs[k - i], in + b * bs, offs[k - i + 1] - offs[k - i],
-                                   hipMemcpyHostToDevice, c->stream));
+        for (auto &p : c->stage_in) BMH_HIP(hipHostMalloc((void **)&p, in_bytes, hipHostMallocDefault));
+        c->stage_in_size = in_bytes;
+    }
+    if (c->stage_out_size < out_bytes) {
+        for (auto &p : c->stage_out) {
+            if (p) BMH_HIP(hipHostFree(p));
+            p = nullptr;
         }
-        uint64_t cap = 0;
-        for (uint32_t k = 0; k < nbk; ++k) cap += record_bound(offs[k + 1] - offs[k]);
-        uint8_t *d_out = (uint8_t *)c->get(WS_OUT, cap);
-        std::vector<uint64_t> ro(nbk + 1);
-        encode_blocks(c, d_in, bt, d_out, cap, ro.data());
-        for (uint32_t k = 0; k < nbk; ++k) {
-            std::vector<uint8_t> r(ro[k + 1] - ro[k]);
-            BMH_HIP(hipMemcpyAsync(r.data(), d_out + ro[k], r.size(), hipMemcpyDeviceToHost, c->stream));
-            recs.push_back(std::move(r));
-        }
-        c->sync();
-        i = j;
+        for (auto &p : c->stage_out) BMH_HIP(hipHostMalloc((void **)&p, out_bytes, hipHostMallocDefault));
+        c->stage_out_size = out_bytes;
     }
 }
 
-static void assemble(uint64_t n, uint64_t bs, uint64_t nblocks, std::vector<std::vector<uint8_t>> &recs, uint8_t *out,
+// Host-buffer encode of blocks `blist` of `in` (block size bs) on one context, pipelined over
+// batches through two staging slots (BASELINE config 5):
+//   loader thread : batch k+1 pageable -> pinned (parallel memcpy), H2D on the h2d stream
+//   this thread   : encode batch k (context streams), then its records D2H on the d2h stream
+//   writer thread : records of batch k-1 pinned -> recs[] (parallel memcpy)
+// so PCIe traffic both ways and the host copies overlap the device encode.
+struct RecRef {
+    const uint8_t *p = nullptr;
+    uint64_t len = 0;
+};
+
+// Receives the records of consecutive entries [i0, i0 + cnt) of the block list: record j at
+// src + ro[j] .. src + ro[j + 1] (pinned staging; valid only during the call).
+using RecordSink = std::function<void(size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro)>;
+
+static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t bs, const std::vector<uint64_t> &blist,
+                               const RecordSink &sink)
+{
+    struct B {
+        std::vector<uint64_t> blocks, offs;
+        uint64_t cap = 0;
+    };
+    const uint64_t cap_batch = stream_batch_bytes();
+    std::vector<B> batches;
+    std::vector<size_t> first;  // block-list index of each batch's first block
+    for (size_t i = 0; i < blist.size();) {
+        first.push_back(i);
+        B bt;
+        bt.offs.push_back(0);
+        size_t j = i;
+        while (j < blist.size()) {
+            const uint64_t len = std::min(bs, n - blist[j] * bs);
+            if (j > i && bt.offs.back() + len > cap_batch) break;
+            bt.blocks.push_back(blist[j]);
+            bt.offs.push_back(bt.offs.back() + len);
+            bt.cap += record_bound(len);
+            ++j;
+        }
+        batches.push_back(std::move(bt));
+        i = j;
+    }
+    const size_t K = batches.size();
+    if (K == 0) return;
+    uint64_t max_in = 0, max_cap = 0;
+    for (auto &bt : batches) {
+        max_in = std::max(max_in, bt.offs.back());
+        max_cap = std::max(max_cap, bt.cap);
+    }
+    ensure_staging(c, max_in, max_cap);
+    uint8_t *d_in[2] = {(uint8_t *)c->get(WS_IN, max_in), (uint8_t *)c->get(WS_IN2, max_in)};
+    uint8_t *d_out[2] = {(uint8_t *)c->get(WS_OUT, max_cap), (uint8_t *)c->get(WS_OUT2, max_cap)};
+    hipEvent_t ev_h2d[2], ev_d2h[2];
+    for (int s = 0; s < 2; ++s) {
+        BMH_HIP(hipEventCreateWithFlags(&ev_h2d[s], hipEventDisableTiming));
+        BMH_HIP(hipEventCreateWithFlags(&ev_d2h[s], hipEventDisableTiming));
+    }
+    const unsigned nt = copy_threads();
+    std::mutex m;
+    std::condition_variable cv;
+    size_t loaded = 0;    // batches whose H2D is issued
+    size_t encoded = 0;   // batches whose encode finished (their input slot is free)
+    size_t written = 0;   // batches whose records left their output slot
+    size_t d2h_issued = 0;
+    bool abort_ = false;
+    std::vector<std::vector<uint64_t>> ro(K);
+    std::string err;
+    bmh_status st = BMH_OK;
+    auto wait_for = [&](auto pred) {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return abort_ || pred(); });
+        return !abort_;
+    };
+    auto bump = [&](size_t &ctr) {
+        std::lock_guard<std::mutex> lk(m);
+        ++ctr;
+        cv.notify_all();
+    };
+    auto fail_all = [&](bmh_status s, const std::string &e) {
+        std::lock_guard<std::mutex> lk(m);
+        if (st == BMH_OK) {
+            st = s;
+            err = e;
+        }
+        abort_ = true;
+        cv.notify_all();
+    };
+    auto guarded = [&](auto fn) {
+        return [&, fn] {
+            try {
+                BMH_HIP(hipSetDevice(c->device));
+                fn();
+            } catch (const Error &e) {
+                fail_all(e.status, e.what());
+            } catch (const std::exception &e) {
+                fail_all(BMH_EHIP, e.what());
+            }
+        };
+    };
+    std::thread loader(guarded([&] {
+        for (size_t k = 0; k < K; ++k) {
+            const int s = (int)(k & 1);
+            if (!wait_for([&] { return encoded + 2 > k; })) return;  // encode k-2 has read d_in[s]
+            if (k >= 2) BMH_HIP(hipEventSynchronize(ev_h2d[s]));     // H2D k-2 has read stage_in[s]
+            const B &bt = batches[k];
+            // consecutive blocks of the input are copied as one run
+            for (size_t i = 0; i < bt.blocks.size();) {
+                size_t j = i + 1;
+                while (j < bt.blocks.size() && bt.blocks[j] == bt.blocks[j - 1] + 1) ++j;
+                par_memcpy(c->stage_in[s] + bt.offs[i], in + bt.blocks[i] * bs, bt.offs[j] - bt.offs[i], nt);
+                i = j;
+            }
+            BMH_HIP(hipMemcpyAsync(d_in[s], c->stage_in[s], bt.offs.back(), hipMemcpyHostToDevice, c->s_h2d));
+            BMH_HIP(hipEventRecord(ev_h2d[s], c->s_h2d));
+            bump(loaded);
+        }
+    }));
+    std::thread writer(guarded([&] {
+        for (size_t k = 0; k < K; ++k) {
+            const int s = (int)(k & 1);
+            if (!wait_for([&] { return d2h_issued > k; })) return;
+            BMH_HIP(hipEventSynchronize(ev_d2h[s]));
+            sink(first[k], batches[k].blocks.size(), c->stage_out[s], ro[k].data());
+            bump(written);
+        }
+    }));
+    guarded([&] {
+        for (size_t k = 0; k < K; ++k) {
+            const int s = (int)(k & 1);
+            if (!wait_for([&] { return loaded > k; })) return;
+            BMH_HIP(hipEventSynchronize(ev_h2d[s]));
+            if (k >= 2) BMH_HIP(hipEventSynchronize(ev_d2h[s]));  // D2H k-2 has read d_out[s]
+            const B &bt = batches[k];
+            Batch b = make_batch(bt.offs.data(), (uint32_t)bt.blocks.size());
+            ro[k].resize(bt.blocks.size() + 1);
+            encode_blocks(c, d_in[s], b, d_out[s], bt.cap, ro[k].data());
+            bump(encoded);
+            if (!wait_for([&] { return written + 2 > k; })) return;  // the writer is done with stage_out[s]
+            BMH_HIP(hipMemcpyAsync(c->stage_out[s], d_out[s], ro[k][bt.blocks.size()], hipMemcpyDeviceToHost,
+                                   c->s_d2h));
+            BMH_HIP(hipEventRecord(ev_d2h[s], c->s_d2h));
+            bump(d2h_issued);
+        }
+    })();
+    loader.join();
+    writer.join();
+    for (int s = 0; s < 2; ++s) {
+        (void)hipEventDestroy(ev_h2d[s]);
+        (void)hipEventDestroy(ev_d2h[s]);
+    }
+    if (st != BMH_OK) fail(st, err);
+}
+
+static void assemble(uint64_t n, uint64_t bs, uint64_t nblocks, const std::vector<RecRef> &recs, uint8_t *out,
                      uint64_t out_cap, uint64_t *out_len)
 {
     uint64_t total = 0;
     if (nblocks == 1) {
-        total = recs[0].size();
+        total = recs[0].len;
         if (total > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
-        memcpy(out, recs[0].data(), total);
+        par_memcpy(out, recs[0].p, total, copy_threads());
     } else {
         total = 32 + 8 * nblocks;
-        for (auto &r : recs) total += r.size();
+        for (auto &r : recs) total += r.len;
         if (total > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
         memcpy(out, kContainerMagic, 8);
         put_u64(out + 8, bs);
         put_u64(out + 16, nblocks);
         put_u64(out + 24, n);
+        std::vector<uint64_t> at(nblocks);
         uint64_t o = 32 + 8 * nblocks;
         for (uint64_t b = 0; b < nblocks; ++b) {
-            put_u64(out + 32 + 8 * b, recs[b].size());
-            memcpy(out + o, recs[b].data(), recs[b].size());
-            o += recs[b].size();
+            put_u64(out + 32 + 8 * b, recs[b].len);
+            at[b] = o;
+            o += recs[b].len;
         }
+        // the records in parallel: contiguous runs of blocks per thread
+        const unsigned nt = copy_threads();
+        std::vector<std::thread> th;
+        const uint64_t per = (nblocks + nt - 1) / nt;
+        for (uint64_t b0 = 0; b0 < nblocks; b0 += per)
+            th.emplace_back([&, b0] {
+                for (uint64_t b = b0; b < std::min(nblocks, b0 + per); ++b) memcpy(out + at[b], recs[b].p, recs[b].len);
+            });
+        for (auto &x : th) x.join();
     }
     *out_len = total;
 }
@@ -474,6 +653,12 @@ void bmh_ctx_destroy(bmh_ctx *c)
     for (int s = 0; s < WS_COUNT_; ++s)
         if (c->ws[s]) (void)hipFree(c->ws[s]);
     if (c->pinned) (void)hipHostFree(c->pinned);
+    for (int s = 0; s < 2; ++s) {
+        if (c->stage_in[s]) (void)hipHostFree(c->stage_in[s]);
+        if (c->stage_out[s]) (void)hipHostFree(c->stage_out[s]);
+    }
+    if (c->s_h2d) (void)hipStreamDestroy(c->s_h2d);
+    if (c->s_d2h) (void)hipStreamDestroy(c->s_d2h);
     for (auto &p : c->pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -627,17 +812,42 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
     const uint64_t bs = (block_size == 0 || block_size >= n) ? n : block_size;
     if (bs >= 0xffffffffull) fail(BMH_ERANGE, "block size must be < 4 GiB - 1");
     const uint64_t nblocks = (n + bs - 1) / bs;
-    std::vector<std::vector<uint8_t>> recs(nblocks);
+    std::vector<RecRef> recs(nblocks);
+    std::vector<std::vector<std::unique_ptr<uint8_t[]>>> store(nctx);
     std::vector<std::string> err(nctx);
+    // one context: records go straight from the staging slots to their place in `out`
+    const bool direct = nctx == 1;
+    const uint64_t table = nblocks == 1 ? 0 : 32 + 8 * nblocks;
+    uint64_t at = table;
+    if (direct && table > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
     std::vector<bmh_status> st(nctx, BMH_OK);
     auto work = [&](uint32_t g) {
         try {
             use_device(ctxs[g]);
             std::vector<uint64_t> bl;
             for (uint64_t b = g; b < nblocks; b += nctx) bl.push_back(b);
-            std::vector<std::vector<uint8_t>> mine;
-            encode_host_blocks(ctxs[g], in, n, bs, bl, mine);
-            for (size_t k = 0; k < bl.size(); ++k) recs[bl[k]] = std::move(mine[k]);
+            if (direct) {
+                encode_host_blocks(ctxs[g], in, n, bs, bl,
+                                   [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
+                                       const uint64_t bytes = ro[cnt];
+                                       if (at + bytes > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
+                                       par_memcpy(out + at, src, bytes, copy_threads());
+                                       for (size_t i = 0; i < cnt; ++i) {
+                                           if (table) put_u64(out + 32 + 8 * (i0 + i), ro[i + 1] - ro[i]);
+                                       }
+                                       at += bytes;
+                                   });
+            } else {
+                encode_host_blocks(ctxs[g], in, n, bs, bl,
+                                   [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
+                                       const uint64_t bytes = ro[cnt];
+                                       std::unique_ptr<uint8_t[]> buf(new uint8_t[std::max<uint64_t>(bytes, 1)]);
+                                       par_memcpy(buf.get(), src, bytes, copy_threads());
+                                       for (size_t i = 0; i < cnt; ++i)
+                                           recs[bl[i0 + i]] = RecRef{buf.get() + ro[i], ro[i + 1] - ro[i]};
+                                       store[g].push_back(std::move(buf));
+                                   });
+            }
         } catch (const Error &e) {
             st[g] = e.status;
             err[g] = e.what();
@@ -655,7 +865,17 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
     }
     for (uint32_t g = 0; g < nctx; ++g)
         if (st[g] != BMH_OK) fail(st[g], err[g]);
-    assemble(n, bs, nblocks, recs, out, out_cap, out_len);
+    if (direct) {
+        if (table) {
+            memcpy(out, kContainerMagic, 8);
+            put_u64(out + 8, bs);
+            put_u64(out + 16, nblocks);
+            put_u64(out + 24, n);
+        }
+        *out_len = at;
+    } else {
+        assemble(n, bs, nblocks, recs, out, out_cap, out_len);
+    }
     API_END
 }
 

@@ -189,6 +189,22 @@ def test_container_roundtrip(ctx):
     assert recs[0] == one
 
 
+def test_streamed_host_compress_many_batches(ctx, monkeypatch):
+    """bmh_compress_host's pipeline (staging slots, side-stream H2D/D2H) over many small
+    batches, one and two contexts: the container equals the per-block device records."""
+    data = synth.zipf_text(9_000_017).tobytes()
+    bs = 1 << 20
+    blocks = [data[i:i + bs] for i in range(0, len(data), bs)]
+    want = ctx.encode_blocks(blocks)
+    for batch in (bs, 3 * bs + 5, 1 << 30):  # 9, 3 and 1 batches
+        monkeypatch.setenv("BMH_STREAM_BATCH", str(batch))
+        out = ctx.compress_bytes(data, block_size=bs)
+        assert bmh.container_records(out) == want, batch
+        multi = bmh.compress_bytes_multi([ctx, bmh.Context(0)], data, bs)
+        assert multi == out, batch
+    assert bmh.decompress_bytes(out) == data
+
+
 # ------------------------------------------------------------------------ GPU decode
 def test_gpu_decode_golden_records(ctx):
     """The reference's own records (Calgary + small known answers) decoded on the GPU."""
