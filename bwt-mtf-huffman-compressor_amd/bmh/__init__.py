@@ -23,7 +23,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libbmh.so")
+LIB_PATH = os.environ.get("BMH_LIB") or os.path.join(PKG_ROOT, "lib", "libbmh.so")
 CLI_PATH = os.path.join(PKG_ROOT, "bin", "bmh")
 
 BMH_OK, BMH_EINVAL, BMH_ENOMEM, BMH_EHIP, BMH_ERANGE, BMH_ECORRUPT, BMH_ENODEV = range(7)

@@ -17,9 +17,11 @@
 //                words above inside c's superword (byte counters in LDS), bits above inside
 //                c's word (one popcount). An access clears one mark and sets the next slot —
 //                O(1) work instead of moving up to 255 list entries; the window is renumbered
-//                every 256 symbols. Stamps are stored as a byte + an "accessed this epoch" bit
-//                (288 B per lane), one-wave workgroups. (tools/microbench/mtf_variants.hip:
-//                4.6 ms per GiB vs 28-40 ms for whole-wave list updates on MI355X.)
+//                every 256 symbols (new slot = marks below the old one). Stamps are stored as a
+//                byte + an "accessed this epoch" bit (368 B of state per lane), one-wave
+//                workgroups, branch-free steps (~34 VALU + 10 LDS ops per symbol; 2.9 ms per
+//                GiB on MI355X, vs 28-40 ms for whole-wave list updates,
+//                tools/microbench/mtf_variants.hip).
 //   4. hist    : freq + first occurrence of each MTF value per block (LDS atomics).
 #include "bmh_internal.h"
 #include "device_util.h"
@@ -32,7 +34,6 @@ namespace {
 
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
-constexpr int kMtfGroup = 2;          // symbols per batched MTF step
 
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
@@ -139,155 +140,147 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__
     }
 }
 
-// Time stamps are 9-bit slots kept as a byte (tm8, the low 8 bits) plus an epoch bit (ep: the
-// symbol was accessed since the last renumbering, i.e. its slot is >= 256): 288 B of LDS per
-// lane instead of 512, so six one-wave workgroups fit a CU instead of four waves. A lane's
-// bytes for symbols 4k..4k+3 share one dword, and dword k of lane l sits at k * kLanes + l
-// (every lane in its own bank).
-__device__ __forceinline__ uint32_t tm8_index(uint32_t c, uint32_t l) { return ((c >> 2) * kLanes + l) * 4 + (c & 3u); }
+// Per-lane encode state, in one LDS array of dword rows; row k of lane l is the dword at
+// byte k * 256 + 4 * l, so every lane stays in its own bank:
+//   rows  0..63  stamp bytes: the low 8 bits of symbol c's slot, byte c & 3 of row c >> 2
+//   rows 64..71  epoch bits : bit 8 of the slot ("accessed since the last renumbering"),
+//                             bit c & 31 of row 64 + (c >> 5)
+//   rows 72..87  slot marks : slot t is some symbol's last access, bit t & 31 of row 72 + (t >> 5)
+//   rows 88..91  word counts: marks in word w, byte w & 3 of row 88 + (w >> 2) (while
+//                             renumbering: marks in the words below w)
+// and, in a VGPR, the marks of each 128-slot superword (byte q of S).
+// 368 B per lane, so six one-wave workgroups fit a CU. Addresses are byte offsets.
+constexpr uint32_t kRowTm = 0, kRowEp = 64, kRowBits = 72, kRowCnt = 88, kRows = 92;
 
-__device__ __forceinline__ uint32_t stamp_read(const uint8_t *tm8, const uint32_t *ep, uint32_t c, uint32_t l)
-{
-    const uint32_t lo = tm8[tm8_index(c, l)];
-    const uint32_t e = ep[(c >> 5) * kLanes + l];
-    return lo | (((e >> (c & 31u)) & 1u) << 8);
-}
+__device__ __forceinline__ uint32_t lds_u32(const uint8_t *s, uint32_t a) { return *(const uint32_t *)(s + a); }
 
-// a new slot (>= 256) for symbol c
-__device__ __forceinline__ void stamp_write_new(uint8_t *tm8, uint32_t *ep, uint32_t c, uint32_t l, uint32_t slot)
+// MTF of symbol c at the wave-uniform slot `now` (the group's first slot now0 is a multiple of
+// 16, k < 16, so all slots of a group share one marks word). Returns the index; the state update
+// (old mark cleared, new mark set, stamp rewritten) happens only for valid symbols.
+template <bool kPred>
+__device__ __forceinline__ uint32_t mtf_step(uint32_t c, bool valid, uint32_t now0, uint32_t k, uint8_t *s, uint32_t l4,
+                                             uint32_t &S)
 {
-    tm8[tm8_index(c, l)] = (uint8_t)slot;
-    atomicOr(&ep[(c >> 5) * kLanes + l], 1u << (c & 31u));
-}
-
-// Marks above slot t: bits above in t's word + words above in t's superword + superwords above.
-__device__ __forceinline__ uint32_t marks_above(uint32_t t, uint32_t S, const uint32_t *bits, const uint32_t *cnt,
-                                                uint32_t l)
-{
-    const uint32_t ws = t >> 5, sb = t & 31u, wq = ws >> 2, wr = ws & 3u;
-    const uint32_t bw = bits[ws * kLanes + l];
-    const uint32_t cw = cnt[wq * kLanes + l];
-    uint32_t r = __builtin_popcount((bw >> sb) >> 1);
-    r = __builtin_amdgcn_sad_u8(cw & (0xFFFFFF00u << (8 * wr)), 0u, r);
-    r = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << (8 * wq)), 0u, r);
+    const uint32_t a8 = (kRowTm << 8) + ((c >> 2) << 8) + l4 + (c & 3u);
+    const uint32_t ae = (kRowEp << 8) + ((c >> 5) << 8) + l4;
+    const uint32_t lo = s[a8];
+    const uint32_t e = lds_u32(s, ae);
+    const uint32_t t = lo | (((e >> (c & 31u)) & 1u) << 8);
+    const uint32_t ab = (kRowBits << 8) + ((t >> 5) << 8) + l4;
+    const uint32_t ac = (kRowCnt << 8) + ((t >> 7) << 8) + l4;
+    const uint32_t bw = lds_u32(s, ab), cw = lds_u32(s, ac);
+    const uint32_t sw = (t >> 2) & 24u, ss = (t >> 4) & 24u;
+    uint32_t r = __builtin_popcount((bw >> (t & 31u)) >> 1);
+    r = __builtin_amdgcn_sad_u8(cw & (0xFFFFFF00u << sw), 0u, r);
+    r = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << ss), 0u, r);
+    if (!kPred || valid) {
+        atomicXor((uint32_t *)(s + ab), 1u << (t & 31u));
+        atomicSub((uint32_t *)(s + ac), 1u << sw);
+        S -= 1u << ss;
+        // the new mark: slot now0 + k (uniform word, bit and counters)
+        const uint32_t nw = now0 >> 5;
+        atomicOr((uint32_t *)(s + (kRowBits << 8) + (nw << 8) + l4), 1u << ((now0 & 31u) + k));
+        atomicAdd((uint32_t *)(s + (kRowCnt << 8) + ((nw >> 2) << 8) + l4), 1u << (8 * (nw & 3u)));
+        S += 1u << (8 * (now0 >> 7));
+        s[a8] = (uint8_t)(now0 + k);
+        atomicOr((uint32_t *)(s + ae), 1u << (c & 31u));
+    }
     return r;
 }
 
-__device__ __forceinline__ void window_reset(uint32_t *bits, uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t &now)
+// Slots 0..255 marked (the start alphabet or the renumbered window), epochs cleared.
+__device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t &S)
 {
-    for (uint32_t w = 0; w < 16; ++w) bits[w * kLanes + l] = w < 8 ? 0xffffffffu : 0u;
-    for (uint32_t q = 0; q < 4; ++q) cnt[q * kLanes + l] = q < 2 ? 0x20202020u : 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) *(uint32_t *)(s + ((kRowBits + w) << 8) + l4) = w < 8 ? 0xffffffffu : 0u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) *(uint32_t *)(s + ((kRowCnt + q) << 8) + l4) = q < 2 ? 0x20202020u : 0u;
+#pragma unroll
+    for (uint32_t w = 0; w < 8; ++w) *(uint32_t *)(s + ((kRowEp + w) << 8) + l4) = 0u;
     S = 0x00008080u;
-    now = 256;
 }
 
-
-// MTF of G consecutive symbols of one lane with ONE round of state reads (batched step).
-// All reads see the state before the group; in registers, for symbol j:
-//   first occurrence in the group: idx = marks above its stamp + #{i < j first in the group
-//                                  whose stamp is below it} (those moved above it);
-//   repeat of position p:          idx = #distinct symbols in (p, j) = popcount of the
-//                                  "latest occurrence" set above p.
-// Then the state update: each first occurrence clears its old mark, each last occurrence
-// takes slot now0 + j (one OR per group: the G slots share a word).
-template <int G>
-__device__ __forceinline__ uint32_t mtf_group(const uint32_t (&c)[G], uint32_t vmask, uint8_t *tm8, uint32_t *ep,
-                                              uint32_t *bits, uint32_t *cnt, uint32_t l, uint32_t &S, uint32_t now0,
-                                              uint32_t (&idx)[G])
+// The window is full (slot 512 reached): every symbol's new slot is the number of marks below
+// its slot (0..255, order kept). The word-count rows are overwritten with the marks below each
+// word first, so a symbol costs two LDS reads and a masked popcount.
+__device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_t &S)
 {
-    uint32_t t[G], base[G], prev[G];
+    uint32_t run = 0, pw[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < G; ++j) t[j] = stamp_read(tm8, ep, c[j], l);
-#pragma unroll
-    for (int j = 0; j < G; ++j) base[j] = marks_above(t[j], S, bits, cnt, l);
-    uint32_t first = 0, lastm = vmask;
-#pragma unroll
-    for (int j = 0; j < G; ++j) {
-        prev[j] = G;
-#pragma unroll
-        for (int i = 0; i < j; ++i)
-            if (((vmask >> i) & 1u) && c[i] == c[j]) prev[j] = i;
-        if (((vmask >> j) & 1u) && prev[j] == G) first |= 1u << j;
-        if (((vmask >> j) & 1u) && prev[j] < G) lastm &= ~(1u << prev[j]);
+    for (uint32_t w = 0; w < 16; ++w) {
+        pw[w >> 2] |= (run & 255u) << (8 * (w & 3u));  // only words holding a mark are read
+        run += __builtin_popcount(lds_u32(s, ((kRowBits + w) << 8) + l4));
     }
-    uint32_t M = 0;  // latest-occurrence positions among the group's symbols so far
 #pragma unroll
-    for (int j = 0; j < G; ++j) {
-        uint32_t r;
-        if ((first >> j) & 1u) {
-            r = base[j];
+    for (uint32_t q = 0; q < 4; ++q) *(uint32_t *)(s + ((kRowCnt + q) << 8) + l4) = pw[q];
+#pragma nounroll
+    for (uint32_t w = 0; w < 8; ++w) {  // symbols 32w .. 32w + 31
+        const uint32_t e = lds_u32(s, ((kRowEp + w) << 8) + l4);
+        uint32_t tw[8];
 #pragma unroll
-            for (int i = 0; i < j; ++i) r += ((first >> i) & 1u) && t[i] < t[j];
-        } else {
-            r = __builtin_popcount(M >> (prev[j] + 1));
-        }
-        idx[j] = r;
-        if ((vmask >> j) & 1u) M = (M & ~(prev[j] < G ? 1u << prev[j] : 0u)) | (1u << j);
-    }
-    // state update: clear the old marks of first occurrences, set the last occurrences' slots
+        for (uint32_t j = 0; j < 8; ++j) tw[j] = lds_u32(s, ((8 * w + j) << 8) + l4);
 #pragma unroll
-    for (int j = 0; j < G; ++j) {
-        if ((first >> j) & 1u) {
-            const uint32_t ws = t[j] >> 5, wq = ws >> 2;
-            atomicXor(&bits[ws * kLanes + l], 1u << (t[j] & 31u));
-            atomicSub(&cnt[wq * kLanes + l], 1u << (8 * (ws & 3u)));
-            S -= 1u << (8 * wq);
+        for (uint32_t j = 0; j < 8; ++j) {
+            uint32_t nwd = 0;
+#pragma unroll
+            for (uint32_t b = 0; b < 4; ++b) {
+                const uint32_t k = 4 * j + b;
+                const uint32_t t = ((tw[j] >> (8 * b)) & 255u) | (((e >> k) & 1u) << 8);
+                const uint32_t below = s[(kRowCnt << 8) + ((t >> 7) << 8) + l4 + ((t >> 5) & 3u)];
+                const uint32_t bw = lds_u32(s, (kRowBits << 8) + ((t >> 5) << 8) + l4);
+                nwd |= (below + __builtin_popcount(bw & ((1u << (t & 31u)) - 1u))) << (8 * b);
+            }
+            *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = nwd;
         }
     }
-    const uint32_t wn = now0 >> 5, np = __builtin_popcount(lastm);
-    atomicOr(&bits[wn * kLanes + l], lastm << (now0 & 31u));
-    atomicAdd(&cnt[(wn >> 2) * kLanes + l], np << (8 * (wn & 3u)));
-    S += np << (8 * (wn >> 2));
-#pragma unroll
-    for (int j = 0; j < G; ++j)
-        if ((lastm >> j) & 1u) stamp_write_new(tm8, ep, c[j], l, now0 + j);
-    return 0;
+    window_reset(s, l4, S);
 }
 
-// grid = ceil(chunks / 256); one lane per chunk. Chunks start 16-byte aligned except a block's
+// Bytes [a, a + 16) of L that lie in [lo, hi), zero elsewhere (chunk edges only).
+__device__ __forceinline__ uint4 load_edge16(const uint8_t *__restrict__ L, uint32_t a, uint32_t lo, uint32_t hi)
+{
+    uint32_t v[4] = {0, 0, 0, 0};
+#pragma nounroll
+    for (uint32_t k = 0; k < 16; ++k)
+        if (a + k >= lo && a + k < hi) v[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// grid = ceil(chunks / 64); one lane per chunk. Chunks start 16-byte aligned except a block's
 // (<= 15-byte) first chunk; all lanes step through 16-symbol groups in lockstep so that the
-// slot counter `now` (and the renumbering every 256 slots) stays wave-uniform; a lane whose
-// group holds fewer than 16 of its symbols predicates the missing steps off (their slots stay
-// unmarked, which is harmless: slots only order accesses).
+// slot counter (and the renumbering every 256 slots) stays wave-uniform. Groups wholly inside
+// the chunk run the branch-free step; edge groups predicate the symbols outside the chunk off
+// (their slots stay unmarked, which is harmless: slots only order accesses).
 __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                        uint32_t nch, const uint32_t *__restrict__ Sst,
                                                        uint8_t *__restrict__ out)
 {
-    __shared__ uint32_t tm32[64 * kLanes];  // the stamp bytes (tm8_index)
-    __shared__ uint32_t ep[8 * kLanes];
-    __shared__ uint32_t bits[16 * kLanes];
-    uint8_t *tm8 = (uint8_t *)tm32;
-    __shared__ uint32_t cnt[4 * kLanes];
-    const uint32_t l = threadIdx.x;
+    __shared__ uint32_t st32[kRows * kLanes];
+    uint8_t *s = (uint8_t *)st32;
+    const uint32_t l = threadIdx.x, l4 = 4 * l;
     const uint32_t g = blockIdx.x * kLanes + l;
     const bool live = g < nch;
     const MChunk ch = live ? chunks[g] : MChunk{0, 0, 0, 0};
-    if (live) {
-        const uint32_t *st = Sst + (size_t)g * 64;
+    if (live) {  // start alphabet: front symbol -> slot 255
+        const uint32_t *stv = Sst + (size_t)g * 64;
         for (uint32_t k4 = 0; k4 < 64; ++k4) {
-            const uint32_t w = st[k4];
-            for (uint32_t j = 0; j < 4; ++j) tm8[tm8_index((w >> (8 * j)) & 255u, l)] = (uint8_t)(255 - (4 * k4 + j));
-        }
-    }
-    for (uint32_t w = 0; w < 8; ++w) ep[w * kLanes + l] = 0;
-    uint32_t S, now;
-    window_reset(bits, cnt, l, S, now);
-    const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
-    const uint32_t ngroups = live ? (((end + 15u) & ~15u) - base) >> 4 : 0u;
-    // the input of group g (16 symbols, zero outside the chunk); fetched two groups ahead
-    auto load_group = [&](uint32_t gi) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        const uint32_t a = base + 16 * gi;
-        if (gi < ngroups) {
-            if (a >= ch.start && a + 16 <= end) {
-                v = *(const uint4 *)(L + a);
-            } else {
-                uint32_t *vw = &v.x;
-                for (uint32_t k = 0; k < 16; ++k)
-                    if (a + k >= ch.start && a + k < end) vw[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
+            const uint32_t w = stv[k4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const uint32_t c = (w >> (8 * j)) & 255u;
+                s[((c >> 2) << 8) + l4 + (c & 3u)] = (uint8_t)(255 - (4 * k4 + j));
             }
         }
-        return v;
+    }
+    uint32_t S, now = 256;
+    window_reset(s, l4, S);
+    const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
+    const uint32_t ngroups = live ? (((end + 15u) & ~15u) - base) >> 4 : 0u;
+    auto load_group = [&](uint32_t gi) {
+        const uint32_t a = base + 16 * gi;
+        if (gi >= ngroups) return make_uint4(0, 0, 0, 0);
+        if (a >= ch.start && a + 16 <= end) return *(const uint4 *)(L + a);
+        return load_edge16(L, a, ch.start, end);
     };
     uint4 pf0 = load_group(0), pf1 = load_group(1);
     for (uint32_t grp = 0; __builtin_amdgcn_ballot_w64(grp < ngroups) != 0; ++grp) {
@@ -296,60 +289,29 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         const uint4 in4 = pf0;
         pf0 = pf1;
         pf1 = load_group(grp + 2);
-        uint4 o4 = make_uint4(0, 0, 0, 0);
-        uint32_t *o = &o4.x;
-        const uint32_t *iw = &in4.x;
-        uint32_t vm = 0;  // symbols of this group that belong to the lane's chunk
-        if (grp < ngroups)
-            for (uint32_t k = 0; k < 16; ++k) vm |= (uint32_t)(a + k >= ch.start && a + k < end) << k;
+        const uint32_t iw[4] = {in4.x, in4.y, in4.z, in4.w};
+        uint32_t o[4] = {0, 0, 0, 0};
+        if (full) {
 #pragma unroll
-        for (int h = 0; h < 16 / kMtfGroup; ++h) {
-            uint32_t cs[kMtfGroup], ix[kMtfGroup];
-#pragma unroll
-            for (int j = 0; j < kMtfGroup; ++j) {
-                const int k = h * kMtfGroup + j;
-                cs[j] = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
+                o[k >> 2] |= mtf_step<false>(c, true, now, k, s, l4, S) << (8 * (k & 3));
             }
-            mtf_group<kMtfGroup>(cs, (vm >> (h * kMtfGroup)) & ((1u << kMtfGroup) - 1), tm8, ep, bits, cnt, l, S, now,
-                                 ix);
+        } else {
 #pragma unroll
-            for (int j = 0; j < kMtfGroup; ++j) {
-                const int k = h * kMtfGroup + j;
-                o[k >> 2] |= (ix[j] & 255u) << (8 * (k & 3));
+            for (uint32_t k = 0; k < 16; ++k) {
+                const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
+                const bool v = grp < ngroups && a + k >= ch.start && a + k < end;
+                o[k >> 2] |= (mtf_step<true>(c, v, now, k, s, l4, S) & 255u) << (8 * (k & 3));
             }
-            now += kMtfGroup;
         }
-        // a group of 16 symbols advances `now` by 16 from 256, so the window fills up
-        // exactly at a group boundary
-        if (now == 512) {  // wave-uniform: renumber slot of each symbol -> 255 - marks above
-            uint32_t e8[8];
-#pragma unroll
-            for (int w = 0; w < 8; ++w) e8[w] = ep[w * kLanes + l];
-            for (uint32_t s0 = 0; s0 < 256; s0 += 16) {  // 16 independent reads in flight
-                uint32_t tw[4], nw[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) tw[k] = tm32[((s0 >> 2) + k) * kLanes + l];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) nw[k] = 0;
-#pragma unroll
-                for (int k = 0; k < 16; ++k) {
-                    const uint32_t c = s0 + k;
-                    uint32_t e = 0;
-#pragma unroll
-                    for (int w = 0; w < 8; ++w)  // c >> 5 is uniform per unrolled step
-                        if ((uint32_t)w == (c >> 5)) e = e8[w];
-                    const uint32_t ts = ((tw[k >> 2] >> (8 * (k & 3))) & 255u) | (((e >> (c & 31u)) & 1u) << 8);
-                    nw[k >> 2] |= (255u - marks_above(ts, S, bits, cnt, l)) << (8 * (k & 3));
-                }
-#pragma unroll
-                for (int k = 0; k < 4; ++k) tm32[((s0 >> 2) + k) * kLanes + l] = nw[k];
-            }
-#pragma unroll
-            for (int w = 0; w < 8; ++w) ep[w * kLanes + l] = 0;
-            window_reset(bits, cnt, l, S, now);
+        now += 16;  // 256 + 16 per group: the window fills up exactly at a group boundary
+        if (now == 512) {
+            window_renumber(s, l4, S);
+            now = 256;
         }
         if (full) {
-            *(uint4 *)(out + a) = o4;
+            *(uint4 *)(out + a) = make_uint4(o[0], o[1], o[2], o[3]);
         } else if (grp < ngroups) {
             for (uint32_t k = 0; k < 16; ++k)
                 if (a + k >= ch.start && a + k < end) out[a + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));

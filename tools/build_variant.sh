@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build an experimental libbmh.so with extra compile flags for ONE source file, linked with the
+# in-tree objects of the others: tools/build_variant.sh <name> <src.hip> <flags...>
+# -> variants/<name>/libbmh.so (git-ignored; load it with BMH_LIB=variants/<name>/libbmh.so).
+set -e
+name=$1; src=$2; shift 2
+root=$(cd "$(dirname "$0")/.." && pwd)
+pkg=$root/bwt-mtf-huffman-compressor_amd
+make -s -C "$pkg" >/dev/null
+out=$root/variants/$name
+mkdir -p "$out"
+base=$(basename "$src")
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I"$root/include" --offload-arch=gfx950 \
+    "$@" -c "$pkg/csrc/$base" -o "$out/$base.o"
+objs=""
+for o in "$pkg"/build/*.o; do
+    [ "$(basename "$o")" = "$base.o" ] && objs="$objs $out/$base.o" || objs="$objs $o"
+done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libbmh.so" $objs
+echo "$out/libbmh.so"
