@@ -270,7 +270,12 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
         g1_load16(blk, ch.start, ch.len, e, dg);
         const uint32_t nv = min(16u, ch.len - e);
         const uint32_t nx = blk[(uint32_t)(((uint64_t)ch.start + e + nv) % n)];
-        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx)], 1u);
+        if (nv == 16) {
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dg, k, 16, nx)], 1u);
+        } else {
+            for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx)], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t d = t; d < kG1Bins; d += 1024)
@@ -311,10 +316,11 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
                                                      const uint32_t *__restrict__ chist, const uint2 *__restrict__ bk,
                                                      uint64_t *__restrict__ rec)
 {
-    __shared__ uint16_t s_ent[kG1Chunk];  // chunk-relative position
+    __shared__ uint16_t s_ent[kG1Chunk + 1];  // chunk-relative position (+ a dummy slot)
     // byte j <-> block position start - 4 + j (cyclic), j < len + 12
     __shared__ uint32_t s_txt[(kG1Chunk + 12) / 4 + 1];
-    __shared__ uint32_t s_cnt[kG1Bins], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
+    __shared__ uint32_t s_cnt[kG1Bins + 1], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
+    // (s_cnt[kG1Bins]: sink digit of the slots past the chunk, so the LDS phases run unbranched)
     __shared__ uint32_t s_tmp[17];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
@@ -359,8 +365,12 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         } else {
             nx = s_txt[(e0 >> 2) + 5] & 255u;
         }
-        for (uint32_t k = 0; k < nv; ++k) atomicAdd(&s_cnt[g1_digit(dg, k, nv, nx)], 1u);
     }
+    uint32_t dgt[16];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) dgt[k] = k < nv ? g1_digit(dg, k, nv, nx) : kG1Bins;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) atomicAdd(&s_cnt[dgt[k]], 1u);
     __syncthreads();
     {
         static_assert(kG1Bins == 1024, "one digit per thread");
@@ -369,11 +379,15 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         s_cnt[t] = ex;
     }
     __syncthreads();
-    for (uint32_t k = 0; k < nv; ++k) {
-        const uint32_t dst = atomicAdd(&s_cnt[g1_digit(dg, k, nv, nx)], 1u);
-        s_ent[dst] = (uint16_t)(e0 + k);
+    {
+        uint32_t dst[16];  // all 16 slot reservations in flight before the first wait
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) dst[k] = atomicAdd(&s_cnt[dgt[k]], 1u);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) s_ent[dgt[k] < kG1Bins ? dst[k] : kG1Chunk] = (uint16_t)(e0 + k);
     }
     __syncthreads();
+#pragma unroll 4
     for (uint32_t i = t; i < ch.len; i += 1024) {
         const uint32_t rel = s_ent[i];
         const uint32_t p = ch.start + rel;
