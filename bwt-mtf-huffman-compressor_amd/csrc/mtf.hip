@@ -82,23 +82,49 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
     if (t == 0) dcount[blockIdx.x] = (uint32_t)d;
 }
 
-// grid = nblocks, one wave each: sequential composition of the chunk recency lists. The
-// recency lists (256 B per chunk) are fetched 32 chunks ahead into registers and parked in
-// LDS, so the sequential chain never waits on global memory.
+// Composition of recency lists. A list R (the distinct symbols of a span, most recent first,
+// d entries) acts on an MTF state as S -> R ++ (S minus R), and two spans compose into a list
+// of the same kind (later ++ (earlier minus later)), so chunk start states come from three
+// short sequential levels instead of one walk over all of a block's chunks:
+//   1. per superchunk (kSuper chunks): compose its chunk lists from the empty state -> the
+//      superchunk's list (its "touched" prefix, d' entries);
+//   2. per block: walk its superchunk lists from the identity alphabet -> each superchunk's
+//      start state;
+//   3. per superchunk: walk its chunk lists from that start -> each chunk's start state.
+// One wave per run; a lane holds state positions 4l .. 4l + 3. The lists are fetched 32 steps
+// ahead into registers and parked in LDS, so the sequential chain never waits on memory.
 constexpr uint32_t kComposeBatch = 32;
+constexpr uint32_t kSuper = 32;  // chunks per superchunk
 
-__global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__ chunk_first,
-                                                    const uint8_t *__restrict__ R, const uint32_t *__restrict__ dcount,
-                                                    uint32_t *__restrict__ S)
+struct CRun {
+    uint32_t c0, c1;  // list indices [c0, c1)
+    uint32_t start;   // start state index (Sin), or kIdentity
+    uint32_t out;     // final list index (Rout / dout)
+};
+constexpr uint32_t kIdentity = 0xffffffffu;
+
+// kSteps: write the state BEFORE each step to Sout[list index]; kFinal: write the final state's
+// touched prefix to Rout[run.out] and its length to dout[run.out].
+template <bool kSteps, bool kFinal>
+__global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ runs, const uint8_t *__restrict__ R,
+                                                    const uint32_t *__restrict__ dcount,
+                                                    const uint32_t *__restrict__ Sin, uint32_t *__restrict__ Sout,
+                                                    uint8_t *__restrict__ Rout, uint32_t *__restrict__ dout)
 {
     __shared__ uint32_t s_R[kComposeBatch][64];
     __shared__ uint32_t s_d[kComposeBatch];
     __shared__ uint8_t s_S[256], s_flag[256];
-    const uint32_t b = blockIdx.x, l = threadIdx.x;
-    const uint32_t c0 = chunk_first[b], c1 = chunk_first[b + 1];
+    const CRun run = runs[blockIdx.x];
+    const uint32_t l = threadIdx.x, c0 = run.c0, c1 = run.c1;
     const uint32_t *R32 = (const uint32_t *)R;
     uint32_t st[4];
-    for (int k = 0; k < 4; ++k) st[k] = 4 * l + k;
+    if (run.start == kIdentity) {
+        for (int k = 0; k < 4; ++k) st[k] = 4 * l + k;
+    } else {
+        const uint32_t w = Sin[(size_t)run.start * 64 + l];
+        for (int k = 0; k < 4; ++k) st[k] = (w >> (8 * k)) & 255u;
+    }
+    uint32_t dt = 0;  // touched prefix of the state (kFinal: the run started empty)
     uint32_t pre[kComposeBatch], pred = 0;
     auto fetch = [&](uint32_t cb) {
 #pragma unroll
@@ -116,18 +142,20 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__
         if (cb + kComposeBatch < c1) fetch(cb + kComposeBatch);
         const uint32_t ce = min(c1, cb + kComposeBatch);
         for (uint32_t c = cb; c < ce; ++c) {
-            S[(size_t)c * 64 + l] = st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
+            if (kSteps) Sout[(size_t)c * 64 + l] = st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
             const uint32_t d = s_d[c - cb], rw = s_R[c - cb][l];
             *(uint32_t *)&s_flag[4 * l] = 0;
             __syncthreads();
             for (uint32_t k = 0; k < 4; ++k)
                 if (4 * l + k < d) s_flag[(rw >> (8 * k)) & 255u] = 1;
             __syncthreads();
-            uint32_t keep[4], cnt = 0;
+            uint32_t keep[4], cnt = 0, kt = 0;
             for (int k = 0; k < 4; ++k) {
                 keep[k] = s_flag[st[k]] == 0;
                 cnt += keep[k];
+                kt += keep[k] && 4 * l + k < dt;
             }
+            if (kFinal) dt = d + wave_sum(kt);
             uint32_t pos = d + wave_incl_sum(cnt) - cnt;
             for (int k = 0; k < 4; ++k)
                 if (keep[k]) s_S[pos++] = (uint8_t)st[k];
@@ -137,6 +165,12 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const uint32_t *__restrict__
             for (int k = 0; k < 4; ++k) st[k] = s_S[4 * l + k];
             __syncthreads();
         }
+    }
+    if (kFinal) {
+        uint8_t *ro = Rout + (size_t)run.out * 256;
+        for (int k = 0; k < 4; ++k)
+            if (4 * l + k < dt) ro[4 * l + k] = (uint8_t)st[k];
+        if (l == 0) dout[run.out] = dt;
     }
 }
 
@@ -403,28 +437,52 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
             hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
     }
     cfirst[nb] = (uint32_t)hc.size();
-    const uint32_t nch = (uint32_t)hc.size(), nhh = (uint32_t)hh.size();
+    // composition runs: superchunks of <= kSuper chunks (levels 1 and 3), blocks (level 2)
+    std::vector<CRun> r1, r2, r3;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint32_t g0 = (uint32_t)r1.size();
+        for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += kSuper) {
+            const uint32_t g = (uint32_t)r1.size(), e = std::min(cfirst[b + 1], x + kSuper);
+            r1.push_back(CRun{x, e, kIdentity, g});
+            r3.push_back(CRun{x, e, g, g});
+        }
+        r2.push_back(CRun{g0, (uint32_t)r1.size(), kIdentity, 0});
+    }
+    const uint32_t nch = (uint32_t)hc.size(), nhh = (uint32_t)hh.size(), ng = (uint32_t)r1.size();
     const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
-    uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + 64);
+    const size_t tr = (2 * (size_t)ng + nb) * sizeof(CRun);
+    uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + tr + 64);
     MChunk *d_chunks = (MChunk *)d_tab;
     HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
     uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));
     uint32_t *d_pfirst = d_cfirst + (nb + 1);
+    CRun *d_r1 = (CRun *)(d_tab + ((tb + 15) & ~(size_t)15)), *d_r3 = d_r1 + ng, *d_r2 = d_r3 + ng;
     c->h2d(d_chunks, hc.data(), nch * sizeof(MChunk));
     c->h2d(d_hh, hh.data(), nhh * sizeof(HChunk));
-    c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
     c->h2d(d_pfirst, pfirst.data(), (nb + 1) * 4);
+    c->h2d(d_r1, r1.data(), ng * sizeof(CRun));
+    c->h2d(d_r3, r3.data(), ng * sizeof(CRun));
+    c->h2d(d_r2, r2.data(), nb * sizeof(CRun));
     uint16_t *d_chist = (uint16_t *)c->get(WS_PACK_HIST, (size_t)pfirst[nb] * 256 * 2 + 64);
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
     uint32_t *d_S = (uint32_t *)c->get(WS_MTF_S, (size_t)nch * 256);
+    uint8_t *d_sup = (uint8_t *)c->get(WS_MTF_SUPER, (size_t)ng * (256 + 256 + 4) + 64);
+    uint8_t *d_Rg = d_sup;                                       // superchunk lists
+    uint32_t *d_Sg = (uint32_t *)(d_sup + (size_t)ng * 256);     // superchunk start states
+    uint32_t *d_dg = (uint32_t *)(d_sup + (size_t)ng * 512);     // superchunk list lengths
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
     BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
     BMH_LAUNCH(c, "mtf_fill", k_fill_u32, (uint32_t)(((size_t)nb * 256 + 255) / 256), 256, 0, d_first, 0xffffffffu,
                (size_t)nb * 256);
     BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, nch, 256, 0, d_L, d_chunks, d_R, d_dcount);
-    BMH_LAUNCH(c, "mtf_compose", k_mtf_compose, nb, 64, 0, d_cfirst, d_R, d_dcount, d_S);
+    BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
+               d_dg);
+    BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), nb, 64, 0, d_r2, d_Rg, d_dg, nullptr, d_Sg, nullptr,
+               nullptr);
+    BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng, 64, 0, d_r3, d_R, d_dcount, d_Sg, d_S, nullptr,
+               nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_pfirst, d_freq, d_first, d_chist);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
