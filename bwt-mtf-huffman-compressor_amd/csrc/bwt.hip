@@ -292,15 +292,31 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
     const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // list indices c0 + 8k (XCD lane stride)
+    // two sweeps over the block's chunk counts (8 loads in flight each): the digit's total,
+    // then, after the block scan, each chunk's write offset
+    constexpr uint32_t U = 8;
+    auto at = [&](uint32_t k) -> uint32_t & { return chist[(size_t)(c0 + 8 * k) * kG1Bins + d]; };
     uint32_t run = 0;
-    for (uint32_t k = 0; k < nc; ++k) {
-        uint32_t *h = &chist[(size_t)(c0 + 8 * k) * kG1Bins + d];
-        const uint32_t v = *h;
-        *h = run;
-        run += v;
+    for (uint32_t k = 0; k < nc; k += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < nc ? at(k + j) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) run += v[j];
     }
     const uint32_t start = block_excl_sum<kG1Bins>(run, s_tmp, nullptr);
-    for (uint32_t k = 0; k < nc; ++k) chist[(size_t)(c0 + 8 * k) * kG1Bins + d] += start;
+    uint32_t acc = start;
+    for (uint32_t k = 0; k < nc; k += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < nc ? at(k + j) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j)
+            if (k + j < nc) {
+                at(k + j) = acc;
+                acc += v[j];
+            }
+    }
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
     if (run > kBigCap)
         big[wave_append(&cnt->big)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
