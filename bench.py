@@ -44,12 +44,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 ALGO_BYTES_PER_INPUT_BYTE = 1.0
 STAGE_BYTES_PER_INPUT_BYTE = {
     "bwt_g1_hist": 1.0,         # read input
-    "bwt_g1_scatter": 13.0,     # read input 1 B, write SA 4 B + rotation key 8 B
-    "bwt_finish_dense": 17.0,   # read SA 4 B + key 8 B, write SA 4 B + L 1 B
+    "bwt_g1_scatter": 9.0,      # read input 1 B, write the 8-byte rotation record
+    "bwt_finish_dense": 9.0,    # read the 8-byte record, write L 1 B
     "mtf_recency": 1.0,         # read L
     "mtf_encode": 2.0,          # read L 1 B, write MTF 1 B
     "mtf_hist": 1.0,            # read MTF
-    "pack_bits": 1.0,           # read MTF
     "pack_write": 2.0,          # read MTF 1 B, write payload ~1 B (random data)
 }
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")

@@ -96,11 +96,13 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ int16_t s_left[512], s_right[512];
     __shared__ uint64_t s_code[256];
     __shared__ uint8_t s_len[256];
-    __shared__ uint8_t s_tree[320];
-    __shared__ uint16_t s_stk_node[260];
-    __shared__ uint8_t s_stk_depth[260];
-    __shared__ uint64_t s_stk_code[260];
-    __shared__ uint32_t s_tree_bits, s_err;
+    __shared__ uint32_t s_tree32[80];                  // tree bytes (320), stream byte i = byte i
+    __shared__ uint16_t s_par[512];                    // parent, then jump target (root: itself)
+    __shared__ uint16_t s_dep[512];                    // path length to the jump target
+    __shared__ uint64_t s_pcode[512];                  // path bits to the jump target (left 0, right 1)
+    __shared__ uint64_t s_lkey[256];                   // leaf codes, left-aligned (preorder order)
+    __shared__ uint32_t s_err;
+    uint8_t *s_tree = (uint8_t *)s_tree32;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
     for (uint32_t s = lane; s < 256; s += 64) {
         s_freq[s] = freq32[(size_t)b * 256 + s];
@@ -108,7 +110,6 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         s_len[s] = 0;
         s_code[s] = 0;
     }
-    for (uint32_t i = lane; i < 320; i += 64) s_tree[i] = 0;
     if (lane == 0) s_err = 0;
     __syncthreads();
     // leaves in first-occurrence order (main.cpp:238-244); first positions are distinct
@@ -149,42 +150,90 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         }
     }
     __syncthreads();
-    // codes (left 0, right 1; a root leaf gets the empty code) and preorder tree bits
-    if (lane == 0) {
-        const uint32_t root = L == 1 ? 0u : 2 * L - 2;
-        uint32_t sp = 0, bit = 0;
-        s_stk_node[0] = (uint16_t)root;
-        s_stk_depth[0] = 0;
-        s_stk_code[0] = 0;
-        sp = 1;
-        while (sp) {
-            --sp;
-            const uint32_t v = s_stk_node[sp], d = s_stk_depth[sp];
-            const uint64_t code = s_stk_code[sp];
-            if (v < L) {
-                const uint32_t sym = s_order[v];
-                if (d > 64) s_err |= kStatusCodeLen;
-                s_len[sym] = (uint8_t)d;
-                s_code[sym] = code;
-                // 0 then the 8 value bits
-                const uint32_t val = sym;
-                bit += 1;
-                for (int k = 7; k >= 0; --k, ++bit)
-                    if ((val >> k) & 1u) s_tree[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7u));
-            } else {
-                s_tree[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7u));
-                ++bit;
-                s_stk_node[sp] = (uint16_t)s_right[v];
-                s_stk_depth[sp] = (uint8_t)(d + 1);
-                s_stk_code[sp] = (code << 1) | 1u;
-                ++sp;
-                s_stk_node[sp] = (uint16_t)s_left[v];
-                s_stk_depth[sp] = (uint8_t)(d + 1);
-                s_stk_code[sp] = code << 1;
-                ++sp;
+    // codes (left 0, right 1; a root leaf gets the empty code) by pointer jumping on parent
+    // links: node x keeps (target a, path bits c, path length d) with code(x) = code(a) << d | c
+    const uint32_t nn = 2 * L - 1;  // nodes; the root (nn - 1) is its own target
+    for (uint32_t v = lane; v < nn; v += 64) {
+        s_par[v] = (uint16_t)v;
+        s_dep[v] = 0;
+        s_pcode[v] = 0;
+    }
+    __syncthreads();
+    for (uint32_t v = L + lane; v < nn; v += 64) {
+        const uint32_t a = (uint32_t)s_left[v], c = (uint32_t)s_right[v];
+        s_par[a] = (uint16_t)v;
+        s_dep[a] = 1;
+        s_par[c] = (uint16_t)v;
+        s_dep[c] = 1;
+        s_pcode[c] = 1;
+    }
+    __syncthreads();
+    for (uint32_t round = 0; round < 9; ++round) {  // depth <= 255 < 2^9
+        uint32_t na[8], nd[8];
+        uint64_t nc[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {  // all reads of the round before any write
+            const uint32_t v = lane + 64 * k;
+            na[k] = v;
+            nd[k] = 0;
+            nc[k] = 0;
+            if (v < nn) {
+                const uint32_t a = s_par[v], d = s_dep[v];
+                const uint64_t c = s_pcode[v];
+                const uint32_t a2 = s_par[a], d2 = s_dep[a];
+                const uint64_t c2 = s_pcode[a];
+                na[k] = a2;
+                nd[k] = d + d2;
+                nc[k] = d >= 64 ? c : (c2 << d) | c;  // (longer paths are flagged below)
             }
         }
-        s_tree_bits = bit;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t v = lane + 64 * k;
+            if (v < nn) {
+                s_par[v] = (uint16_t)na[k];
+                s_dep[v] = (uint16_t)min(nd[k], 0xffffu);
+                s_pcode[v] = nc[k];
+            }
+        }
+        __syncthreads();
+    }
+    // leaves: code book, and the left-aligned codes, whose order is the preorder of the leaves
+    for (uint32_t v = lane; v < L; v += 64) {
+        const uint32_t d = s_dep[v], sym = s_order[v];
+        if (d > 64) atomicOr(&s_err, kStatusCodeLen);
+        const uint64_t code = d > 64 ? 0ull : s_pcode[v];
+        s_len[sym] = (uint8_t)min(d, 255u);
+        s_code[sym] = code;
+        s_lkey[v] = d == 0 ? 0ull : d > 64 ? ~0ull : code << (64 - d);
+    }
+    // preorder tree bits (tree_to_bytes main.cpp:174-196): all 10L - 1 bits start as internal
+    // '1's; leaf j in preorder (j leaves and depth + j - popcount(code) internal nodes before
+    // it) owns bits [10j + depth - popcount, +9): a '0' then its 8 value bits MSB-first
+    const uint32_t tbits = 10 * L - 1;
+    for (uint32_t w = lane; w < 80; w += 64) {
+        uint32_t x = 0;
+        for (uint32_t k = 0; k < 32; ++k) {
+            const uint32_t bit = 32 * w + 8 * (k >> 3) + (7 - (k & 7));  // stream bit of u32 bit k
+            if (bit < tbits) x |= 1u << k;
+        }
+        s_tree32[w] = x;
+    }
+    __syncthreads();
+    for (uint32_t v = lane; v < L; v += 64) {
+        const uint64_t key = s_lkey[v];
+        uint32_t j = 0;
+        for (uint32_t u = 0; u < L; ++u) j += s_lkey[u] < key;
+        const uint32_t d = s_dep[v], sym = s_order[v];
+        const uint32_t off = 10 * j + min(d, 64u) - (uint32_t)__builtin_popcountll(s_pcode[v]);
+        for (uint32_t i = 0; i < 9; ++i) {
+            const uint32_t one = i == 0 ? 0u : (sym >> (8 - i)) & 1u;
+            if (!one) {
+                const uint32_t pbit = off + i, byte = pbit >> 3;
+                atomicAnd(&s_tree32[byte >> 2], ~(1u << (8 * (byte & 3) + 7 - (pbit & 7))));
+            }
+        }
     }
     __syncthreads();
     DevTable *t = &tabs[b];
@@ -195,7 +244,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         bits += (uint64_t)s_freq[s] * s_len[s];
     }
     for (int off = 32; off >= 1; off >>= 1) bits += __shfl_xor(bits, off, 64);
-    const uint32_t tree_len = (s_tree_bits + 7) >> 3;
+    const uint32_t tree_len = (tbits + 7) >> 3;
     const uint64_t n = boffs[b + 1] - boffs[b];
     const uint32_t p = prim[b];
     uint8_t *h = hdr + (size_t)b * kHdrStride;
