@@ -9,9 +9,9 @@
 //              0..L-1, internal nodes L, L+1, ... in creation order; a pop takes the
 //              smallest (freq, -addr_rank(id)) — equal frequencies leave the heap in
 //              descending glibc heap-address order (same model as
-//              huffman_host.cpp). Each pop is a wave-wide argmin over 512 register slots.
-//   codes    : DFS from the root (left = 0), preorder tree bits (internal 1, leaf 0 + 8
-//              value bits MSB-first), by lane 0.
+//              huffman_host.cpp) — run as two queues (sorted leaves, internal-node groups).
+//   codes    : pointer jumping on parent links (left = 0); preorder tree bits (internal 1,
+//              leaf 0 + 8 value bits MSB-first) placed per leaf in parallel.
 //   header   : [u64 primary][u64 n][u64 tree_len][tree bytes] staged per block.
 // k_rec_offs then scans header + payload sizes into record offsets (capacity checked on the
 // device), and k_rec_headers copies each header to its record.
@@ -45,42 +45,30 @@ __device__ __forceinline__ uint32_t addr_rank(uint32_t L, uint32_t s)
     return s;
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v)
-{
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-
+// Priority-queue key of node id (pop order = ascending key): frequency, then descending
+// heap-address rank, then the id itself in the low bits (never decides: ranks are distinct).
 __device__ __forceinline__ uint64_t heap_key(uint64_t freq, uint32_t L, uint32_t id)
 {
-    return (freq << 32) | (0xffffu - addr_rank(L, id));
+    return (freq << 32) | ((0xffffu - addr_rank(L, id)) << 16) | id;
 }
 
-// Removes the minimum key of the wave's 512 slots; returns its node id and frequency.
-__device__ __forceinline__ uint32_t heap_pop(uint64_t (&key)[8], uint64_t &freq)
+// Rank of each of this lane's keys (slots lane + 64k) among the 256 keys of s_keys (padding
+// entries ~0): the number of smaller keys. Keys are read two at a time, 8 loads in flight.
+__device__ __forceinline__ void rank4_u64(const uint64_t *s_keys, uint32_t lane, uint32_t (&pos)[4])
 {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint64_t lm = key[0];
+    uint64_t mine[4];
 #pragma unroll
-    for (int k = 1; k < 8; ++k) lm = key[k] < lm ? key[k] : lm;
-    const uint64_t wm = wave_min_u64(lm);
-    uint32_t myid = 0;
-    bool found = false;
+    for (int k = 0; k < 4; ++k) {
+        mine[k] = s_keys[lane + 64 * k];
+        pos[k] = 0;
+    }
+#pragma unroll 8
+    for (uint32_t u = 0; u < 256; u += 2) {
+        const uint4 v = *(const uint4 *)&s_keys[u];
+        const uint64_t a = ((uint64_t)v.y << 32) | v.x, c = ((uint64_t)v.w << 32) | v.z;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (key[k] == wm) {
-            key[k] = ~0ull;
-            myid = lane + 64u * k;
-            found = true;
-        }
-    const uint64_t bal = __ballot(found);
-    const int owner = __ffsll((long long)bal) - 1;
-    freq = wm >> 32;
-    return (uint32_t)__shfl((int)myid, owner, 64);
+        for (int k = 0; k < 4; ++k) pos[k] += (uint32_t)(a < mine[k]) + (uint32_t)(c < mine[k]);
+    }
 }
 
 // grid = nblocks, 64 threads (one wave per block).
@@ -100,7 +88,8 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ uint16_t s_par[512];                    // parent, then jump target (root: itself)
     __shared__ uint16_t s_dep[512];                    // path length to the jump target
     __shared__ uint64_t s_pcode[512];                  // path bits to the jump target (left 0, right 1)
-    __shared__ uint64_t s_lkey[256];                   // leaf codes, left-aligned (preorder order)
+    __shared__ uint64_t s_lkey[256];                   // leaf keys, then left-aligned leaf codes
+    __shared__ uint64_t s_k1[256], s_q2[256];          // leaves in pop order; internal-node queue
     __shared__ uint32_t s_err;
     uint8_t *s_tree = (uint8_t *)s_tree32;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -116,37 +105,81 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     uint32_t L = 0;
     for (uint32_t s = lane; s < 256; s += 64) L += s_freq[s] > 0;
     for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
-    for (uint32_t s = lane; s < 256; s += 64) {
-        if (!s_freq[s]) continue;
-        const uint32_t fs = s_first[s];
-        uint32_t r = 0;
-        for (uint32_t t = 0; t < 256; ++t) r += s_freq[t] > 0 && s_first[t] < fs;
-        s_order[r] = (uint8_t)s;
+    for (uint32_t s = lane; s < 256; s += 64) s_lkey[s] = s_freq[s] ? s_first[s] : ~0ull;
+    __syncthreads();
+    {
+        uint32_t pos[4];
+        rank4_u64(s_lkey, lane, pos);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (s_freq[lane + 64 * k]) s_order[pos[k]] = (uint8_t)(lane + 64 * k);
     }
     __syncthreads();
     if (L == 0) {
         if (lane == 0) atomicOr(status, kStatusEmpty);
         return;
     }
-    // the priority queue (main.cpp:245-254): first pop -> left child, second -> right
-    uint64_t key[8];
+    // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
+    // two queues: the leaves sorted by key, and the internal nodes, which are created with
+    // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is
+    // a run of frequency groups, each popped newest first (the larger rank of an equal
+    // frequency pops first). Exactly the heap's pop order, O(1) per pop, on lane 0.
+    for (uint32_t id = lane; id < 256; id += 64) s_lkey[id] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
+    __syncthreads();
+    {
+        uint32_t pos[4];
+        rank4_u64(s_lkey, lane, pos);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t id = lane + 64u * k;
-        key[k] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
+        for (int k = 0; k < 4; ++k)
+            if (lane + 64 * k < L) s_k1[pos[k]] = s_lkey[lane + 64 * k];
     }
-    for (uint32_t m = 0; m + 1 < L; ++m) {
-        uint64_t fa, fb;
-        const uint32_t a = heap_pop(key, fa);
-        const uint32_t c = heap_pop(key, fb);
-        const uint32_t v = L + m;
-        const uint64_t nk = heap_key(fa + fb, L, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (lane + 64u * k == v) key[k] = nk;
-        if (lane == 0) {
-            s_left[v] = (int16_t)a;
-            s_right[v] = (int16_t)c;
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t q1 = 0;                      // next leaf
+        uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
+        uint64_t k1 = s_k1[0], k2 = ~0ull;    // queue heads (k2 = s_q2[ge - 1])
+        uint32_t gf = 0;                      // first group's frequency
+        auto pop = [&]() -> uint64_t {
+            uint64_t r;
+            if (k1 < k2) {
+                r = k1;
+                ++q1;
+                k1 = q1 < L ? s_k1[q1] : ~0ull;
+            } else {
+                r = k2;
+                --ge;
+                if (ge > gh) {
+                    k2 = s_q2[ge - 1];
+                } else {  // the first group is used up: the next one starts at gn
+                    gh = gn;
+                    ge = gh;
+                    k2 = ~0ull;
+                    if (gh < me) {
+                        gf = (uint32_t)(s_q2[gh] >> 32);
+                        while (ge < me && (uint32_t)(s_q2[ge] >> 32) == gf) ++ge;
+                        gn = ge;
+                        k2 = s_q2[ge - 1];
+                    }
+                }
+            }
+            return r;
+        };
+        for (uint32_t m = 0; m + 1 < L; ++m) {
+            const uint64_t ra = pop(), rb = pop();
+            const uint32_t v = L + m;
+            const uint64_t f = (ra >> 32) + (rb >> 32);
+            s_left[v] = (int16_t)(ra & 0xffffu);
+            s_right[v] = (int16_t)(rb & 0xffffu);
+            const uint64_t nk = heap_key(f, L, v);
+            if (gn == me && (ge == gh || (uint32_t)f == gf)) {
+                // the queue is empty, or the node joins the last (= first) group: it pops first
+                if (ge == gh) gf = (uint32_t)f;
+                s_q2[ge++] = nk;
+                if (ge > gn) gn = me = ge;
+                k2 = nk;
+            } else {
+                s_q2[me++] = nk;  // a later group
+            }
         }
     }
     __syncthreads();
@@ -200,7 +233,11 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         __syncthreads();
     }
     // leaves: code book, and the left-aligned codes, whose order is the preorder of the leaves
-    for (uint32_t v = lane; v < L; v += 64) {
+    for (uint32_t v = lane; v < 256; v += 64) {
+        if (v >= L) {
+            s_lkey[v] = ~0ull;
+            continue;
+        }
         const uint32_t d = s_dep[v], sym = s_order[v];
         if (d > 64) atomicOr(&s_err, kStatusCodeLen);
         const uint64_t code = d > 64 ? 0ull : s_pcode[v];
@@ -221,10 +258,12 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         s_tree32[w] = x;
     }
     __syncthreads();
-    for (uint32_t v = lane; v < L; v += 64) {
-        const uint64_t key = s_lkey[v];
-        uint32_t j = 0;
-        for (uint32_t u = 0; u < L; ++u) j += s_lkey[u] < key;
+    uint32_t jpos[4];
+    rank4_u64(s_lkey, lane, jpos);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t v = lane + 64 * k, j = jpos[k];
+        if (v >= L) continue;
         const uint32_t d = s_dep[v], sym = s_order[v];
         const uint32_t off = 10 * j + min(d, 64u) - (uint32_t)__builtin_popcountll(s_pcode[v]);
         for (uint32_t i = 0; i < 9; ++i) {
