@@ -270,21 +270,13 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
     window_reset(s, l4, S);
 }
 
-// Bytes [a, a + 16) of L that lie in [lo, hi), zero elsewhere (chunk edges only).
-__device__ __forceinline__ uint4 load_edge16(const uint8_t *__restrict__ L, uint32_t a, uint32_t lo, uint32_t hi)
-{
-    uint32_t v[4] = {0, 0, 0, 0};
-#pragma nounroll
-    for (uint32_t k = 0; k < 16; ++k)
-        if (a + k >= lo && a + k < hi) v[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
-    return make_uint4(v[0], v[1], v[2], v[3]);
-}
-
-// grid = ceil(chunks / 64); one lane per chunk. Chunks start 16-byte aligned except a block's
-// (<= 15-byte) first chunk; all lanes step through 16-symbol groups in lockstep so that the
-// slot counter (and the renumbering every 256 slots) stays wave-uniform. Groups wholly inside
-// the chunk run the branch-free step; edge groups predicate the symbols outside the chunk off
-// (their slots stay unmarked, which is harmless: slots only order accesses).
+// grid = ceil(chunks / 64); one lane per chunk. Chunks start 64-byte aligned except a block's
+// (<= 63-byte) first chunk; all lanes step through 64-symbol super-groups in lockstep so that
+// the slot counter (and the renumbering every 256 slots = every 4 super-groups) stays
+// wave-uniform. A super-group wholly inside the chunk is loaded and stored as one 64-byte
+// sector per lane (four 16-byte accesses back to back) and runs the branch-free step; edge
+// super-groups predicate the symbols outside the chunk off (their slots stay unmarked, which is
+// harmless: slots only order accesses).
 __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                        uint32_t nch, const uint32_t *__restrict__ Sst,
                                                        uint8_t *__restrict__ out)
@@ -308,47 +300,68 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
     }
     uint32_t S, now = 256;
     window_reset(s, l4, S);
-    const uint32_t base = ch.start & ~15u, end = ch.start + ch.len;
-    const uint32_t ngroups = live ? (((end + 15u) & ~15u) - base) >> 4 : 0u;
-    auto load_group = [&](uint32_t gi) {
-        const uint32_t a = base + 16 * gi;
-        if (gi >= ngroups) return make_uint4(0, 0, 0, 0);
-        if (a >= ch.start && a + 16 <= end) return *(const uint4 *)(L + a);
-        return load_edge16(L, a, ch.start, end);
+    const uint32_t base = ch.start & ~63u, end = ch.start + ch.len;
+    const uint32_t nsg = live ? (((end + 63u) & ~63u) - base) >> 6 : 0u;
+    auto whole = [&](uint32_t gi) {
+        const uint32_t a = base + 64 * gi;
+        return gi < nsg && a >= ch.start && a + 64 <= end;
     };
-    uint4 pf0 = load_group(0), pf1 = load_group(1);
-    for (uint32_t grp = 0; __builtin_amdgcn_ballot_w64(grp < ngroups) != 0; ++grp) {
-        const uint32_t a = base + 16 * grp;
-        const bool full = grp < ngroups && a >= ch.start && a + 16 <= end;
-        const uint4 in4 = pf0;
-        pf0 = pf1;
-        pf1 = load_group(grp + 2);
-        const uint32_t iw[4] = {in4.x, in4.y, in4.z, in4.w};
-        uint32_t o[4] = {0, 0, 0, 0};
-        if (full) {
+    auto load_sg = [&](uint32_t gi, uint4 (&v)[4]) {
+        if (whole(gi)) {
+            const uint4 *p = (const uint4 *)(L + base + 64 * gi);
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) {
-                const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
-                o[k >> 2] |= mtf_step<false>(c, true, now, k, s, l4, S) << (8 * (k & 3));
-            }
+            for (int q = 0; q < 4; ++q) v[q] = p[q];
         } else {
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) {
-                const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
-                const bool v = grp < ngroups && a + k >= ch.start && a + k < end;
-                o[k >> 2] |= (mtf_step<true>(c, v, now, k, s, l4, S) & 255u) << (8 * (k & 3));
+            for (int q = 0; q < 4; ++q) v[q] = make_uint4(0, 0, 0, 0);
+        }
+    };
+    uint4 pf[4];
+    load_sg(0, pf);
+    for (uint32_t sg = 0; __builtin_amdgcn_ballot_w64(sg < nsg) != 0; ++sg) {
+        const uint32_t a0 = base + 64 * sg;
+        uint4 in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) in[q] = pf[q];
+        load_sg(sg + 1, pf);
+        if (whole(sg)) {
+            uint4 o4[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t iw[4] = {in[q].x, in[q].y, in[q].z, in[q].w};
+                uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) {
+                    const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
+                    o[k >> 2] |= mtf_step<false>(c, true, now + 16 * q, k, s, l4, S) << (8 * (k & 3));
+                }
+                o4[q] = make_uint4(o[0], o[1], o[2], o[3]);
+            }
+            uint4 *po = (uint4 *)(out + a0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) po[q] = o4[q];
+        } else if (sg < nsg) {  // an edge super-group: symbols outside the chunk predicated off
+#pragma nounroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t a = a0 + 16 * q;
+                uint32_t iw[4] = {0, 0, 0, 0};
+                for (uint32_t k = 0; k < 16; ++k)
+                    if (a + k >= ch.start && a + k < end) iw[k >> 2] |= (uint32_t)L[a + k] << (8 * (k & 3));
+                uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) {
+                    const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
+                    const bool v = a + k >= ch.start && a + k < end;
+                    o[k >> 2] |= (mtf_step<true>(c, v, now + 16 * q, k, s, l4, S) & 255u) << (8 * (k & 3));
+                }
+                for (uint32_t k = 0; k < 16; ++k)
+                    if (a + k >= ch.start && a + k < end) out[a + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
             }
         }
-        now += 16;  // 256 + 16 per group: the window fills up exactly at a group boundary
+        now += 64;  // 256 + 64 per super-group: the window fills up exactly at a boundary
         if (now == 512) {
             window_renumber(s, l4, S);
             now = 256;
-        }
-        if (full) {
-            *(uint4 *)(out + a) = make_uint4(o[0], o[1], o[2], o[3]);
-        } else if (grp < ngroups) {
-            for (uint32_t k = 0; k < 16; ++k)
-                if (a + k >= ch.start && a + k < end) out[a + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
         }
     }
 }
@@ -419,11 +432,11 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     for (uint32_t b = 0; b < nb; ++b) {
         cfirst[b] = (uint32_t)hc.size();
         const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
-        // chunk boundaries on 16-byte multiples of the batch (a block's first chunk takes the
-        // unaligned prefix) so the encode kernel moves 16 symbols per vector load / store
+        // chunk boundaries on 64-byte multiples of the batch (a block's first chunk takes the
+        // unaligned prefix) so the encode kernel moves whole 64-byte sectors per lane
         for (uint64_t s = 0; s < n;) {
             const uint64_t gpos = o + s;
-            const uint64_t lim = (gpos & 15u) ? ((gpos + 15) & ~15ull) : gpos + kMtfChunk;
+            const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + kMtfChunk;
             const uint64_t e = std::min<uint64_t>(o + n, lim);
             MChunk m;
             m.block = b;
