@@ -39,47 +39,68 @@ struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
 };
 
-// grid = chunks; 256 threads x 16 symbols. R[c][0..d) = distinct symbols, most recent last
-// occurrence first.
+// One wave per chunk (four per workgroup, no workgroup barriers), lane l owns positions
+// [64l, 64l + 64) loaded as one 64-byte sector. R[c][0..d) = distinct symbols, most recent last
+// occurrence first: LDS atomicMax of positions, a bitset of last-occurrence positions, then each
+// set bit's rank = set bits above it (wave scan).
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
-                                                     uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
+                                                     uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
 {
-    __shared__ int lastpos[256];
-    __shared__ uint32_t bset[kMtfChunk / 32];
-    __shared__ uint32_t s_tmp[8];
-    const MChunk ch = chunks[blockIdx.x];
-    const uint32_t t = threadIdx.x;
-    lastpos[t] = -1;
-    if (t < kMtfChunk / 32) bset[t] = 0;
-    // this thread's 16 symbols (zero past the chunk), one vector load when aligned
-    uint32_t sw[4] = {0, 0, 0, 0};
-    const uint32_t e0 = 16 * t;
-    const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
-    if (nv == 16 && ((ch.start + e0) & 15u) == 0) {
-        const uint4 v = *(const uint4 *)(L + ch.start + e0);
-        sw[0] = v.x;
-        sw[1] = v.y;
-        sw[2] = v.z;
-        sw[3] = v.w;
+    __shared__ int lastpos[4][256];
+    __shared__ uint32_t bset[4][kMtfChunk / 32];
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u, c = blockIdx.x * 4 + w;
+    if (c >= nch) return;  // the whole wave
+    const MChunk ch = chunks[c];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lastpos[w][4 * l + k] = -1;
+    bset[w][2 * l] = 0;
+    bset[w][2 * l + 1] = 0;
+    uint32_t sw[16];
+    const uint32_t e0 = 64 * l;
+    const uint32_t nv = e0 < ch.len ? min(64u, ch.len - e0) : 0u;
+    if (nv == 64 && ((ch.start + e0) & 15u) == 0) {
+        const uint4 *p = (const uint4 *)(L + ch.start + e0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[q];
+            sw[4 * q] = v.x;
+            sw[4 * q + 1] = v.y;
+            sw[4 * q + 2] = v.z;
+            sw[4 * q + 3] = v.w;
+        }
     } else {
-        for (uint32_t k = 0; k < nv; ++k) sw[k >> 2] |= (uint32_t)L[ch.start + e0 + k] << (8 * (k & 3));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sw[q] = 0;
+        for (uint32_t k = 0; k < nv; ++k) {
+            const uint32_t x = (uint32_t)L[ch.start + e0 + k] << (8 * (k & 3));
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if ((uint32_t)q == (k >> 2)) sw[q] |= x;
+        }
     }
-    __syncthreads();
-    for (uint32_t k = 0; k < nv; ++k) atomicMax(&lastpos[(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
-    __syncthreads();
-    const int lp = lastpos[t];
-    if (lp >= 0) atomicOr(&bset[lp >> 5], 1u << (lp & 31));
-    const int d = __syncthreads_count(lp >= 0);
-    // thread t owns positions [16t, 16t+16); ranks count set bits at higher positions
-    const uint32_t v = (bset[t >> 1] >> (16 * (t & 1))) & 0xffffu;
-    const uint32_t cnt = __builtin_popcount(v);
-    uint32_t total;
-    const uint32_t ex = block_excl_sum<256>(cnt, s_tmp, &total);  // set bits in threads < t
-    uint32_t off = total - ex - cnt;                               // set bits in threads > t
-    uint8_t *Rc = R + (size_t)blockIdx.x * 256;
-    for (int b = 15; b >= 0; --b)
-        if (v & (1u << b)) Rc[off++] = (uint8_t)(sw[b >> 2] >> (8 * (b & 3)));
-    if (t == 0) dcount[blockIdx.x] = (uint32_t)d;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (uint32_t k = 0; k < 64; ++k)
+        if (k < nv) atomicMax(&lastpos[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
+    __builtin_amdgcn_wave_barrier();
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int lp = lastpos[w][4 * l + k];
+        if (lp >= 0) atomicOr(&bset[w][lp >> 5], 1u << (lp & 31));
+        d += lp >= 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    d = wave_sum(d);
+    const uint64_t v = ((uint64_t)bset[w][2 * l + 1] << 32) | bset[w][2 * l];
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(v);
+    const uint32_t inc = wave_incl_sum(cnt);
+    uint32_t off = d - inc;  // set bits in lanes above this one
+    uint8_t *Rc = R + (size_t)c * 256;
+#pragma unroll
+    for (int b = 63; b >= 0; --b)
+        if ((v >> b) & 1u) Rc[off++] = (uint8_t)(sw[b >> 2] >> (8 * (b & 3)));
+    if (l == 0) dcount[c] = d;
 }
 
 // Composition of recency lists. A list R (the distinct symbols of a span, most recent first,
@@ -370,54 +391,103 @@ struct HChunk {
     uint32_t block, start, len, rel;
 };
 
-// freq + first occurrence of each MTF value, per block (huffman() main.cpp:231-244), and the
-// histogram of every 4 K-symbol pack chunk (u16; the pack sizes its chunks from these
-// instead of re-reading the MTF stream). One workgroup per 64 K symbols of a block.
-__global__ __launch_bounds__(256) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
-                                                  const uint32_t *__restrict__ pfirst, uint32_t *__restrict__ freq,
-                                                  uint32_t *__restrict__ first, uint16_t *__restrict__ chist)
+// freq of each MTF value per block (huffman() main.cpp:231-237) and the histogram of every
+// 4 K-symbol pack chunk (u16; the pack sizes its chunks from these instead of re-reading the
+// MTF stream). One workgroup per 64 K symbols of a block; wave w takes pack chunk w (lane l:
+// symbols [64l, 64l + 64), one 64-byte sector) with its own LDS histogram, no workgroup
+// barrier until the block totals. First occurrences come from k_mtf_first.
+__global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
+                                                   const uint32_t *__restrict__ pfirst, uint32_t *__restrict__ freq,
+                                                   uint16_t *__restrict__ chist)
 {
-    __shared__ uint32_t h[4][256], f[256];
+    constexpr uint32_t NW = 65536 / kPackChunkSyms;
+    __shared__ uint32_t h[NW][256];
     const HChunk ch = chunks[blockIdx.x];
-    const uint32_t t = threadIdx.x, w = t >> 6;
-    f[t] = 0xffffffffu;
-    uint32_t tot = 0;
-    for (uint32_t s0 = 0; s0 < ch.len; s0 += kPackChunkSyms) {
-        for (int k = 0; k < 4; ++k) h[k][t] = 0;
-        __syncthreads();
-        const uint32_t len = min(kPackChunkSyms, ch.len - s0), a = ch.start + s0;
-        if (len == kPackChunkSyms && (a & 15u) == 0) {
-            const uint4 v4 = *(const uint4 *)(in + a + 16 * t);
-            const uint32_t *vw = &v4.x;
+    const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
+    const uint32_t s0 = w * kPackChunkSyms;
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) {
-                const uint32_t v = (vw[k >> 2] >> (8 * (k & 3))) & 255u, pos = ch.rel + s0 + 16 * t + k;
+    for (int k = 0; k < 4; ++k) h[w][4 * l + k] = 0;
+    if (s0 < ch.len) {
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t len = min(kPackChunkSyms, ch.len - s0), a = ch.start + s0, e0 = 64 * l;
+        if (len == kPackChunkSyms && ((a + e0) & 15u) == 0) {
+            uint32_t sw[16];
+            const uint4 *p = (const uint4 *)(in + a + e0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = p[q];
+                sw[4 * q] = v.x;
+                sw[4 * q + 1] = v.y;
+                sw[4 * q + 2] = v.z;
+                sw[4 * q + 3] = v.w;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 64; ++k) {
+                const uint32_t v = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
                 atomicAdd(&h[w][v], 1u);
-                if (pos < f[v]) atomicMin(&f[v], pos);  // racy read only skips non-minima
             }
         } else {
-            for (uint32_t i = t; i < len; i += 256) {
-                const uint32_t v = in[a + i], pos = ch.rel + s0 + i;
-                atomicAdd(&h[w][v], 1u);
-                if (pos < f[v]) atomicMin(&f[v], pos);
-            }
+            for (uint32_t k = 0; k < 64 && e0 + k < len; ++k) atomicAdd(&h[w][in[a + e0 + k]], 1u);
         }
-        __syncthreads();
-        const uint32_t c = h[0][t] + h[1][t] + h[2][t] + h[3][t];
-        tot += c;
-        chist[(size_t)(pfirst[ch.block] + ((ch.rel + s0) / kPackChunkSyms)) * 256 + t] = (uint16_t)c;
-        __syncthreads();
+        __builtin_amdgcn_wave_barrier();
+        uint16_t *co = chist + (size_t)(pfirst[ch.block] + (ch.rel + s0) / kPackChunkSyms) * 256;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) co[4 * l + k] = (uint16_t)h[w][4 * l + k];
     }
-    if (tot) {
-        atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
-        atomicMin(&first[(size_t)ch.block * 256 + t], f[t]);
+    __syncthreads();
+    if (t < 256) {
+        uint32_t tot = 0;
+#pragma unroll
+        for (uint32_t x = 0; x < NW; ++x) tot += h[x][t];
+        if (tot) atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
     }
 }
 
-__global__ void k_fill_u32(uint32_t *p, uint32_t v, size_t n)
+// First occurrence of each MTF value per block (huffman() main.cpp:238-244 orders the leaves
+// by it). The pack-chunk histograms say in which chunk each value first appears (value v:
+// the first chunk with a nonzero count, found 16 chunks per step); only those chunks are
+// scanned, once per distinct first chunk (on random data: the block's first chunk alone).
+__global__ __launch_bounds__(256) void k_mtf_first(const uint8_t *__restrict__ in, const uint32_t *__restrict__ boffs,
+                                                   const uint32_t *__restrict__ pfirst, const uint32_t *__restrict__ freq,
+                                                   const uint16_t *__restrict__ chist, uint32_t *__restrict__ first)
 {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
+    __shared__ uint32_t f[256], s_cv[256], s_min[5];
+    const uint32_t b = blockIdx.x, v = threadIdx.x;
+    const uint32_t c0 = pfirst[b], nc = pfirst[b + 1] - c0;
+    const uint32_t o = boffs[b], n = boffs[b + 1] - o;
+    f[v] = 0xffffffffu;
+    uint32_t cv = 0xffffffffu;  // first chunk holding v (block-relative); none for absent values
+    bool look = freq[(size_t)b * 256 + v] != 0;
+    for (uint32_t base = 0; __syncthreads_or(look && base < nc); base += 16) {
+        if (!look) continue;
+        uint32_t cnt[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + v] : 0u;
+#pragma unroll
+        for (int j = 15; j >= 0; --j)
+            if (cnt[j]) cv = base + j;
+        look = cv == 0xffffffffu;
+    }
+    s_cv[v] = cv;
+    uint32_t todo = cv;
+    for (;;) {  // the distinct first chunks, smallest first
+        uint32_t m = todo;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off, 64));
+        if ((v & 63u) == 0) s_min[v >> 6] = m;
+        __syncthreads();
+        const uint32_t cm = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
+        __syncthreads();
+        if (cm == 0xffffffffu) break;
+        const uint32_t p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
+        for (uint32_t i = v; i < len; i += 256) {
+            const uint32_t x = in[o + p0 + i];
+            if (s_cv[x] == cm) atomicMin(&f[x], p0 + i);
+        }
+        if (todo == cm) todo = 0xffffffffu;
+    }
+    __syncthreads();
+    first[(size_t)b * 256 + v] = f[v];
 }
 
 }  // namespace
@@ -467,12 +537,17 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + tr + 64);
     MChunk *d_chunks = (MChunk *)d_tab;
     HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
-    uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));
+    uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));  // block offsets
     uint32_t *d_pfirst = d_cfirst + (nb + 1);
     CRun *d_r1 = (CRun *)(d_tab + ((tb + 15) & ~(size_t)15)), *d_r3 = d_r1 + ng, *d_r2 = d_r3 + ng;
     c->h2d(d_chunks, hc.data(), nch * sizeof(MChunk));
     c->h2d(d_hh, hh.data(), nhh * sizeof(HChunk));
     c->h2d(d_pfirst, pfirst.data(), (nb + 1) * 4);
+    {
+        std::vector<uint32_t> bo(nb + 1);
+        for (uint32_t b = 0; b <= nb; ++b) bo[b] = (uint32_t)bt.offs[b];
+        c->h2d(d_cfirst, bo.data(), (nb + 1) * 4);
+    }
     c->h2d(d_r1, r1.data(), ng * sizeof(CRun));
     c->h2d(d_r3, r3.data(), ng * sizeof(CRun));
     c->h2d(d_r2, r2.data(), nb * sizeof(CRun));
@@ -487,9 +562,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
     BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
-    BMH_LAUNCH(c, "mtf_fill", k_fill_u32, (uint32_t)(((size_t)nb * 256 + 255) / 256), 256, 0, d_first, 0xffffffffu,
-               (size_t)nb * 256);
-    BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, nch, 256, 0, d_L, d_chunks, d_R, d_dcount);
+    BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
                d_dg);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), nb, 64, 0, d_r2, d_Rg, d_dg, nullptr, d_Sg, nullptr,
@@ -497,7 +570,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng, 64, 0, d_r3, d_R, d_dcount, d_Sg, d_S, nullptr,
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
-    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 256, 0, d_mtf, d_hh, d_pfirst, d_freq, d_first, d_chist);
+    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist);
+    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, 256, 0, d_mtf, d_cfirst, d_pfirst, d_freq, d_chist, d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     if (h_freq32 || h_first32) c->sync();
