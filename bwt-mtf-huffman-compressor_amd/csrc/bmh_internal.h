@@ -63,6 +63,11 @@ struct Ctx {
     std::vector<hipEvent_t> event_pool;
     void *ws[WS_COUNT_] = {};
     size_t ws_size[WS_COUNT_] = {};
+    // host-built tables kept in a workspace slot: signature of what was uploaded (0 = none or
+    // overwritten; get() clears it on reallocation) and a few counts derived with it, so a
+    // batch with the same layout as the previous one skips the rebuild and the upload
+    uint64_t ws_tag[WS_COUNT_] = {};
+    uint32_t ws_aux[WS_COUNT_][4] = {};
     // pinned host staging
     void *pinned = nullptr;
     size_t pinned_size = 0;
@@ -96,6 +101,22 @@ struct Ctx {
     int tbegin(const char *name);  // -1 when timing is off
     void tend(int idx);
 };
+
+// Signature of a batch layout for the table cache (Ctx::ws_tag): kind, block offsets and the
+// input's 16-byte misalignment (chunk boundaries depend on it).
+inline uint64_t layout_sig(uint64_t kind, const std::vector<uint64_t> &offs, uintptr_t base)
+{
+    uint64_t h = 1469598103934665603ull ^ kind;
+    auto mix = [&](uint64_t v) {
+        h ^= v;
+        h *= 1099511628211ull;
+        h ^= h >> 29;
+    };
+    mix(offs.size());
+    mix(base & 63u);
+    for (uint64_t o : offs) mix(o);
+    return h | 1u;  // never 0
+}
 
 // Host wall-clock of a phase (device work included when the phase synchronises), recorded
 // under "wall:<name>" when timing is enabled.

@@ -1443,36 +1443,42 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
     WallPhase wall_data(c, "bwt_data");
 
-    // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8)
-    std::vector<uint32_t> hoffs(nb + 1);
-    for (uint32_t b = 0; b <= nb; ++b) hoffs[b] = (uint32_t)bt.offs[b];
-    std::vector<std::vector<GChunk>> lane(8);
-    for (uint32_t b = 0; b < nb; ++b) {
-        // the first chunk takes the unaligned prefix so the others start on 16-byte addresses
-        const uint32_t n = hoffs[b + 1] - hoffs[b];
-        const uint32_t mis = (uint32_t)(((uintptr_t)d_in + hoffs[b]) & 15u);
-        uint32_t s = 0, l = std::min(n, kG1Chunk - mis);
-        while (s < n) {
-            lane[b & 7].push_back(GChunk{b, s, l, 0});
-            s += l;
-            l = std::min(n - s, kG1Chunk);
+    // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8); the table is
+    // rebuilt and uploaded only when the batch layout changed since this context's last batch
+    const uint64_t sig = layout_sig(1, bt.offs, (uintptr_t)d_in);
+    uint32_t nchunks;
+    uint8_t *d_tab;
+    if (c->ws_tag[WS_BLOCKS] == sig) {
+        nchunks = c->ws_aux[WS_BLOCKS][0];
+        d_tab = (uint8_t *)c->ws[WS_BLOCKS];
+    } else {
+        std::vector<uint32_t> hoffs(nb + 1);
+        for (uint32_t b = 0; b <= nb; ++b) hoffs[b] = (uint32_t)bt.offs[b];
+        std::vector<std::vector<GChunk>> lane(8);
+        for (uint32_t b = 0; b < nb; ++b) {
+            // the first chunk takes the unaligned prefix so the others start on 16-byte addresses
+            const uint32_t n = hoffs[b + 1] - hoffs[b];
+            const uint32_t mis = (uint32_t)(((uintptr_t)d_in + hoffs[b]) & 15u);
+            uint32_t s = 0, l = std::min(n, kG1Chunk - mis);
+            while (s < n) {
+                lane[b & 7].push_back(GChunk{b, s, l, 0});
+                s += l;
+                l = std::min(n - s, kG1Chunk);
+            }
         }
-    }
-    size_t lmax = 0;
-    for (auto &l : lane) lmax = std::max(lmax, l.size());
-    std::vector<GChunk> chunks(lmax * 8, GChunk{0, 0, 0, 0});
-    std::vector<uint32_t> bchunks(nb, 0), bchunk0(nb, 0);
-    for (uint32_t x = 0; x < 8; ++x)
-        for (size_t k = 0; k < lane[x].size(); ++k) {
-            const GChunk &g = lane[x][k];
-            chunks[k * 8 + x] = g;
-            if (bchunks[g.block]++ == 0) bchunk0[g.block] = (uint32_t)(k * 8 + x);
-        }
-    const uint32_t nchunks = (uint32_t)chunks.size();
-
-    const size_t tab_bytes = (nb + 1) * 4 + nb * 8 + nchunks * sizeof(GChunk);
-    uint8_t *d_tab = (uint8_t *)c->get(WS_BLOCKS, tab_bytes + 64);
-    {
+        size_t lmax = 0;
+        for (auto &l : lane) lmax = std::max(lmax, l.size());
+        std::vector<GChunk> chunks(lmax * 8, GChunk{0, 0, 0, 0});
+        std::vector<uint32_t> bchunks(nb, 0), bchunk0(nb, 0);
+        for (uint32_t x = 0; x < 8; ++x)
+            for (size_t k = 0; k < lane[x].size(); ++k) {
+                const GChunk &g = lane[x][k];
+                chunks[k * 8 + x] = g;
+                if (bchunks[g.block]++ == 0) bchunk0[g.block] = (uint32_t)(k * 8 + x);
+            }
+        nchunks = (uint32_t)chunks.size();
+        const size_t tab_bytes = (nb + 1) * 4 + nb * 8 + nchunks * sizeof(GChunk);
+        d_tab = (uint8_t *)c->get(WS_BLOCKS, tab_bytes + 64);
         std::vector<uint8_t> h(tab_bytes);
         size_t o = 0;
         memcpy(&h[o], hoffs.data(), (nb + 1) * 4);
@@ -1483,7 +1489,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         o += nb * 4;
         memcpy(&h[o], chunks.data(), nchunks * sizeof(GChunk));
         c->h2d(d_tab, h.data(), tab_bytes);
-        c->sync();
+        c->ws_tag[WS_BLOCKS] = sig;
+        c->ws_aux[WS_BLOCKS][0] = nchunks;
     }
     const uint32_t *d_boffs = (const uint32_t *)d_tab;
     const uint32_t *d_bchunks = d_boffs + (nb + 1);

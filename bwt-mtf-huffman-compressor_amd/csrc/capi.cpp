@@ -28,6 +28,7 @@ void *Ctx::get(Slot s, size_t bytes)
 {
     if (bytes == 0) bytes = 1;
     if (ws_size[s] >= bytes) return ws[s];
+    ws_tag[s] = 0;
     if (ws[s]) {
         BMH_HIP(hipStreamSynchronize(stream));
         BMH_HIP(hipFree(ws[s]));

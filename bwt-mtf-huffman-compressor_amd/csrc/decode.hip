@@ -876,6 +876,7 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
 
     // ---- device tables
     DBlock *d_blk = (DBlock *)c->get(WS_BLOCKS, nb * sizeof(DBlock) + 64);
+    c->ws_tag[WS_BLOCKS] = c->ws_tag[WS_MTF_CHUNKS] = 0;  // the encode's cached tables are overwritten
     DecTable *d_tab = (DecTable *)c->get(WS_TABLES, nb * sizeof(DecTable) + 64);
     uint8_t *d_meta = (uint8_t *)c->get(WS_MTF_CHUNKS, (size_t)(nseg + nsp + nch) * 4 + nch * sizeof(IChunk) + 256);
     uint32_t *d_seg_block = (uint32_t *)d_meta;

@@ -495,63 +495,92 @@ __global__ __launch_bounds__(256) void k_mtf_first(const uint8_t *__restrict__ i
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32, uint32_t *h_first32)
 {
     const uint32_t nb = bt.nblocks;
-    std::vector<MChunk> hc;
-    std::vector<HChunk> hh;
-    std::vector<uint32_t> cfirst(nb + 1), pfirst(nb + 1);
-    pack_chunk_first(bt, pfirst.data());
-    for (uint32_t b = 0; b < nb; ++b) {
-        cfirst[b] = (uint32_t)hc.size();
-        const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
-        // chunk boundaries on 64-byte multiples of the batch (a block's first chunk takes the
-        // unaligned prefix) so the encode kernel moves whole 64-byte sectors per lane
-        for (uint64_t s = 0; s < n;) {
-            const uint64_t gpos = o + s;
-            const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + kMtfChunk;
-            const uint64_t e = std::min<uint64_t>(o + n, lim);
-            MChunk m;
-            m.block = b;
-            m.start = (uint32_t)gpos;
-            m.len = (uint32_t)(e - gpos);
-            m.rel = (uint32_t)s;
-            hc.push_back(m);
-            s = e - o;
+    // chunk / composition tables: rebuilt and uploaded only when the batch layout changed
+    const uint64_t sig = layout_sig(2, bt.offs, 0);
+    uint32_t nch, nhh, ng, npk;
+    if (c->ws_tag[WS_MTF_CHUNKS] == sig) {
+        nch = c->ws_aux[WS_MTF_CHUNKS][0];
+        nhh = c->ws_aux[WS_MTF_CHUNKS][1];
+        ng = c->ws_aux[WS_MTF_CHUNKS][2];
+        npk = c->ws_aux[WS_MTF_CHUNKS][3];
+    } else {
+        std::vector<MChunk> hc;
+        std::vector<HChunk> hh;
+        std::vector<uint32_t> cfirst(nb + 1), pfirst(nb + 1);
+        pack_chunk_first(bt, pfirst.data());
+        for (uint32_t b = 0; b < nb; ++b) {
+            cfirst[b] = (uint32_t)hc.size();
+            const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
+            // chunk boundaries on 64-byte multiples of the batch (a block's first chunk takes the
+            // unaligned prefix) so the encode kernel moves whole 64-byte sectors per lane
+            for (uint64_t s = 0; s < n;) {
+                const uint64_t gpos = o + s;
+                const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + kMtfChunk;
+                const uint64_t e = std::min<uint64_t>(o + n, lim);
+                MChunk m;
+                m.block = b;
+                m.start = (uint32_t)gpos;
+                m.len = (uint32_t)(e - gpos);
+                m.rel = (uint32_t)s;
+                hc.push_back(m);
+                s = e - o;
+            }
+            for (uint64_t s = 0; s < n; s += 65536)
+                hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
         }
-        for (uint64_t s = 0; s < n; s += 65536)
-            hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
-    }
-    cfirst[nb] = (uint32_t)hc.size();
-    // composition runs: superchunks of <= kSuper chunks (levels 1 and 3), blocks (level 2)
-    std::vector<CRun> r1, r2, r3;
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint32_t g0 = (uint32_t)r1.size();
-        for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += kSuper) {
-            const uint32_t g = (uint32_t)r1.size(), e = std::min(cfirst[b + 1], x + kSuper);
-            r1.push_back(CRun{x, e, kIdentity, g});
-            r3.push_back(CRun{x, e, g, g});
+        cfirst[nb] = (uint32_t)hc.size();
+        // composition runs: superchunks of <= kSuper chunks (levels 1 and 3), blocks (level 2)
+        std::vector<CRun> r1, r2, r3;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t g0 = (uint32_t)r1.size();
+            for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += kSuper) {
+                const uint32_t g = (uint32_t)r1.size(), e = std::min(cfirst[b + 1], x + kSuper);
+                r1.push_back(CRun{x, e, kIdentity, g});
+                r3.push_back(CRun{x, e, g, g});
+            }
+            r2.push_back(CRun{g0, (uint32_t)r1.size(), kIdentity, 0});
         }
-        r2.push_back(CRun{g0, (uint32_t)r1.size(), kIdentity, 0});
+        nch = (uint32_t)hc.size();
+        nhh = (uint32_t)hh.size();
+        ng = (uint32_t)r1.size();
+        npk = pfirst[nb];
+        // one staged upload: chunks | 64 K pieces | block offsets | pack-chunk firsts | runs
+        const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
+        const size_t tbo = (tb + 15) & ~(size_t)15;
+        const size_t tall = tbo + (2 * (size_t)ng + nb) * sizeof(CRun);
+        std::vector<uint8_t> h(tall, 0);
+        size_t o = 0;
+        memcpy(&h[o], hc.data(), nch * sizeof(MChunk));
+        o += nch * sizeof(MChunk);
+        memcpy(&h[o], hh.data(), nhh * sizeof(HChunk));
+        o += nhh * sizeof(HChunk);
+        for (uint32_t b = 0; b <= nb; ++b, o += 4) {
+            const uint32_t v = (uint32_t)bt.offs[b];
+            memcpy(&h[o], &v, 4);
+        }
+        memcpy(&h[o], pfirst.data(), (nb + 1) * 4);
+        o = tbo;
+        memcpy(&h[o], r1.data(), ng * sizeof(CRun));
+        o += ng * sizeof(CRun);
+        memcpy(&h[o], r3.data(), ng * sizeof(CRun));
+        o += ng * sizeof(CRun);
+        memcpy(&h[o], r2.data(), nb * sizeof(CRun));
+        uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tall + 64);
+        c->h2d(d_tab, h.data(), tall);
+        c->ws_tag[WS_MTF_CHUNKS] = sig;
+        c->ws_aux[WS_MTF_CHUNKS][0] = nch;
+        c->ws_aux[WS_MTF_CHUNKS][1] = nhh;
+        c->ws_aux[WS_MTF_CHUNKS][2] = ng;
+        c->ws_aux[WS_MTF_CHUNKS][3] = npk;
     }
-    const uint32_t nch = (uint32_t)hc.size(), nhh = (uint32_t)hh.size(), ng = (uint32_t)r1.size();
     const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
-    const size_t tr = (2 * (size_t)ng + nb) * sizeof(CRun);
-    uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tb + tr + 64);
+    uint8_t *d_tab = (uint8_t *)c->ws[WS_MTF_CHUNKS];
     MChunk *d_chunks = (MChunk *)d_tab;
     HChunk *d_hh = (HChunk *)(d_tab + nch * sizeof(MChunk));
-    uint32_t *d_cfirst = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));  // block offsets
-    uint32_t *d_pfirst = d_cfirst + (nb + 1);
+    uint32_t *d_boffs = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));  // block offsets
+    uint32_t *d_pfirst = d_boffs + (nb + 1);
     CRun *d_r1 = (CRun *)(d_tab + ((tb + 15) & ~(size_t)15)), *d_r3 = d_r1 + ng, *d_r2 = d_r3 + ng;
-    c->h2d(d_chunks, hc.data(), nch * sizeof(MChunk));
-    c->h2d(d_hh, hh.data(), nhh * sizeof(HChunk));
-    c->h2d(d_pfirst, pfirst.data(), (nb + 1) * 4);
-    {
-        std::vector<uint32_t> bo(nb + 1);
-        for (uint32_t b = 0; b <= nb; ++b) bo[b] = (uint32_t)bt.offs[b];
-        c->h2d(d_cfirst, bo.data(), (nb + 1) * 4);
-    }
-    c->h2d(d_r1, r1.data(), ng * sizeof(CRun));
-    c->h2d(d_r3, r3.data(), ng * sizeof(CRun));
-    c->h2d(d_r2, r2.data(), nb * sizeof(CRun));
-    uint16_t *d_chist = (uint16_t *)c->get(WS_PACK_HIST, (size_t)pfirst[nb] * 256 * 2 + 64);
+    uint16_t *d_chist = (uint16_t *)c->get(WS_PACK_HIST, (size_t)npk * 256 * 2 + 64);
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
     uint32_t *d_S = (uint32_t *)c->get(WS_MTF_S, (size_t)nch * 256);
@@ -571,7 +600,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist);
-    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, 256, 0, d_mtf, d_cfirst, d_pfirst, d_freq, d_chist, d_first);
+    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, 256, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist, d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     if (h_freq32 || h_first32) c->sync();

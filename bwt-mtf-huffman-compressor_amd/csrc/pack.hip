@@ -243,6 +243,7 @@ void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_f
     }
     const uint32_t nch = (uint32_t)hc.size();
     uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 8 + 64);
+    c->ws_tag[WS_PACK_CHUNKS] = 0;  // the pack's cached table is overwritten
     PChunk *d_chunks = (PChunk *)d_meta;
     uint64_t *d_offs = (uint64_t *)(d_meta + ((nch * sizeof(PChunk) + 15) & ~(size_t)15));
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
@@ -263,28 +264,38 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
 {
     if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const uint32_t nb = bt.nblocks;
-    std::vector<PChunk> hc;
-    std::vector<uint32_t> cfirst(nb + 1);
-    for (uint32_t b = 0; b < nb; ++b) {
-        cfirst[b] = (uint32_t)hc.size();
-        const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
-        for (uint64_t s = 0; s < n; s += kPackChunk) {
-            PChunk p;
-            p.block = b;
-            p.start = (uint32_t)(o + s);
-            p.len = (uint32_t)std::min<uint64_t>(kPackChunk, n - s);
-            p.pad = 0;
-            hc.push_back(p);
+    // chunk table: rebuilt and uploaded only when the batch layout changed
+    const uint64_t sig = layout_sig(3, bt.offs, 0);
+    uint32_t nch;
+    if (c->ws_tag[WS_PACK_CHUNKS] == sig) {
+        nch = c->ws_aux[WS_PACK_CHUNKS][0];
+    } else {
+        std::vector<PChunk> hc;
+        std::vector<uint32_t> cfirst(nb + 1);
+        for (uint32_t b = 0; b < nb; ++b) {
+            cfirst[b] = (uint32_t)hc.size();
+            const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
+            for (uint64_t s = 0; s < n; s += kPackChunk) {
+                PChunk p;
+                p.block = b;
+                p.start = (uint32_t)(o + s);
+                p.len = (uint32_t)std::min<uint64_t>(kPackChunk, n - s);
+                p.pad = 0;
+                hc.push_back(p);
+            }
         }
+        cfirst[nb] = (uint32_t)hc.size();
+        nch = (uint32_t)hc.size();
+        uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 4 + 64);
+        c->h2d(d_meta, hc.data(), nch * sizeof(PChunk));
+        c->h2d(d_meta + nch * sizeof(PChunk), cfirst.data(), (nb + 1) * 4);
+        c->ws_tag[WS_PACK_CHUNKS] = sig;
+        c->ws_aux[WS_PACK_CHUNKS][0] = nch;
     }
-    cfirst[nb] = (uint32_t)hc.size();
-    const uint32_t nch = (uint32_t)hc.size();
-    uint8_t *d_meta = (uint8_t *)c->get(WS_PACK_CHUNKS, nch * sizeof(PChunk) + (nb + 1) * 4 + 64);
+    uint8_t *d_meta = (uint8_t *)c->ws[WS_PACK_CHUNKS];
     PChunk *d_chunks = (PChunk *)d_meta;
     uint32_t *d_cfirst = (uint32_t *)(d_meta + nch * sizeof(PChunk));
     uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
-    c->h2d(d_chunks, hc.data(), nch * sizeof(PChunk));
-    c->h2d(d_cfirst, cfirst.data(), (nb + 1) * 4);
     if (d_chist)
         BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(nch, 4), 256, 0, d_chist, d_chunks, nch, d_tabs, d_cbits);
     else
