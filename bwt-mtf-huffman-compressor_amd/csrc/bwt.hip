@@ -514,26 +514,34 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
             }
             continue;
         }
-        uint32_t lt = 0, eqb = 0, eqt = 1;
+        // rank = #(rest, slot) pairs below this element's (one 64-bit compare per member;
+        // sub-buckets hold ~1-4 rotations on random data); ties in the rest are rare and get
+        // a second pass for their group's start
+        uint32_t c = 0, eqt = 1;
+        const uint32_t r = rv[k];
         if (m > 1) {
-            const uint32_t r = rv[k];
+            const uint64_t key = ((uint64_t)r << 32) | me;
             eqt = 0;
 #pragma nounroll
-            for (uint32_t f = s0; f < s1; ++f) {  // sub-buckets are short (~1-4 on random data)
+            for (uint32_t f = s0; f < s1; ++f) {
                 const uint32_t rf = s_rest[f];
-                lt += rf < r;
-                const bool eq = rf == r;
-                eqt += eq;
-                eqb += eq && f < me;
+                c += ((((uint64_t)rf) << 32) | f) < key;
+                eqt += rf == r;
             }
         }
-        const uint32_t local = s0 + lt + eqb, gs = gstart + s0 + lt;
-        if (eqt > 1 && eqb == 0) {  // tied so far
-            dq_push(a, dq, gs, eqt, (uint32_t)newbits, b, n);
-            s_tmp[NT / 64 + 1] = 1;
+        const uint32_t local = s0 + c;
+        uint32_t gs = gstart + local;
+        if (eqt > 1) {  // tied so far: the group starts after the strictly smaller rests
+            uint32_t lt = 0;
+            for (uint32_t f = s0; f < s1; ++f) lt += s_rest[f] < r;
+            gs = gstart + s0 + lt;
+            if (c == lt) {  // the group's first slot pushes it
+                dq_push(a, dq, gs, eqt, (uint32_t)newbits, b, n);
+                s_tmp[NT / 64 + 1] = 1;
+            }
         }
         dd[k] = local;  // dd now holds the element's slot in the segment
-        if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = (eqt == 1 ? gstart + local : gs) - boff;
+        if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = gs - boff;
     }
     dq_flush<NT>(a, dq);
     // slot -> position (<< 8 | L); a slot whose rotation is not final yet gets its L
