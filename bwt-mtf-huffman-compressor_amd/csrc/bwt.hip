@@ -41,6 +41,7 @@ constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
 constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kFinNT = 256, kFinCap = 4096;
+constexpr uint32_t kFinSNT = 128, kFinSCap = 512;  // list segments <= 512 take a small-LDS sort
 constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
@@ -676,7 +677,6 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
-constexpr uint32_t kSortQ = 1024;  // deferral queue of k_finish_sort (overlays its key array)
 
 // List segments (lo < len <= CAP) sorted by their whole next 64 rotation bits: bitonic sort of
 // (window, position) pairs in LDS, then runs of equal windows become the next round's tie
@@ -687,7 +687,8 @@ template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
 {
     static_assert((CAP & (CAP - 1)) == 0, "bitonic capacity");
-    static_assert(sizeof(DeferQueue<kSortQ>) <= CAP * 8, "deferral queue overlays the windows");
+    constexpr uint32_t Q = CAP / 4;  // deferral queue entries (the queue overlays the key array)
+    static_assert(sizeof(DeferQueue<Q>) <= CAP * 8, "deferral queue overlays the windows");
     __shared__ __align__(16) uint64_t s_key[CAP];
     __shared__ uint32_t s_pos[CAP];
     __shared__ uint32_t s_tail[CAP / 32];
@@ -764,7 +765,7 @@ __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__re
     }
     // the windows are no longer needed: their LDS holds the deferral queue
     __syncthreads();
-    DeferQueue<kSortQ> &dq = *reinterpret_cast<DeferQueue<kSortQ> *>(s_key);
+    DeferQueue<Q> &dq = *reinterpret_cast<DeferQueue<Q> *>(s_key);
     dq_init(dq);
     __syncthreads();
 #pragma unroll
@@ -1613,7 +1614,10 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             set_lists(fint_nxt, fin_nxt, finb_nxt, big_nxt);
             if (nfint > 0)
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4 * kTinyPerWave), 256, 0, da, fint_cur, nfint);
-            if (nfin > 0) BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, 1u);
+            if (nfin > 0) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), nfin, kFinSNT, 0, da, fin_cur, 1u);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, kFinSCap);
+            }
             if (nfinb > 0)
                 BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfinb, kBigNT, 0, da, finb_cur, kFinCap);
             if (nbig > 0) {
