@@ -570,47 +570,76 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
     __syncthreads();
 }
 
-// Tiny list segments (len <= kTinyFin): one wave each, lane = element, ranked by the next 64
-// rotation bits with wave shuffles (tie groups of 2-3 rotations are the common case). Each
-// wave takes kTinyPerWave segments so that a workgroup's deferrals share one reservation.
-constexpr uint32_t kTinyPerWave = 8;
-
+// Tiny list segments (len <= kTinyFin), packed: each wave takes 64 consecutive list entries
+// and lays their rotations side by side over its lanes in rounds of <= 64 (a segment never
+// splits across rounds); each rotation is ranked inside its segment by the next 64 rotation
+// bits with wave shuffles. Tie groups of 2-5 rotations are the common case on text, so a wave
+// per segment would leave most lanes idle.
 __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list, uint32_t nlist)
 {
     __shared__ DeferQueue<kDeferQ> dq;
     dq_init(dq);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-    for (uint32_t k = 0; k < kTinyPerWave; ++k) {
-        const uint32_t i = (blockIdx.x * kTinyPerWave + k) * 4 + w;
-        if (i >= nlist) break;  // the whole wave
-        const Seg4 sg = list[i];
-        const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
-        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-        const uint8_t *blk = a.data + boff;
-        uint32_t p = 0;
-        uint64_t key = ~0ull;
-        if (l < len) {
-            p = a.sa[gstart + l];
-            key = rot_window(blk, n, p, db);
-        }
-        uint32_t lt = 0, eqb = 0, eqt = 0;
-        for (uint32_t j = 0; j < len; ++j) {
-            const uint32_t klo = __shfl((uint32_t)key, (int)j, 64), khi = __shfl((uint32_t)(key >> 32), (int)j, 64);
-            const uint64_t kj = ((uint64_t)khi << 32) | klo;
-            lt += kj < key;
-            eqt += kj == key;
-            eqb += kj == key && j < l;
-        }
-        if (l >= len) continue;
-        const uint64_t newbits = (uint64_t)db + 64;
-        const bool final_depth = newbits >= 8ull * n;
-        const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
-        if (eqt > 1 && eqb == 0) dq_push(a, dq, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
-        a.sa[slot] = p;
-        if (eqt == 1 || final_depth) {
-            a.L[slot] = lastcol_byte(blk, n, p);
-            if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+    const uint32_t i0 = (blockIdx.x * 4 + w) * 64;
+    if (i0 < nlist) {  // wave-uniform
+        const Seg4 sgl = i0 + l < nlist ? list[i0 + l] : make_uint4(0, 0, 0, 0);
+        const uint32_t incl = wave_incl_sum(sgl.y), st = incl - sgl.y;
+        const uint32_t total = __shfl(incl, 63, 64);
+        for (uint32_t base = 0; base < total;) {  // wave-uniform rounds
+            // the round: the run of segments from `base` that fits in 64 lanes
+            const bool in = sgl.y > 0 && st >= base && incl <= base + 64;
+            const uint64_t inm = __ballot(in), afterm = __ballot(sgl.y > 0 && st >= base && incl > base + 64);
+            const uint32_t s0 = (uint32_t)__ffsll((unsigned long long)inm) - 1;
+            const uint32_t nbase = afterm ? (uint32_t)__shfl((int)st, __ffsll((unsigned long long)afterm) - 1, 64) : total;
+            uint64_t B = in ? 1ull << (st - base) : 0ull;  // segment starts inside the round
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) B |= __shfl_xor(B, off, 64);
+            const bool live = l < nbase - base;
+            const uint64_t below = l == 63 ? B : B & ((2ull << l) - 1);
+            const uint32_t pos = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;  // my segment's first lane
+            const uint32_t sl = s0 + (uint32_t)__builtin_popcountll(B & ((1ull << pos) - 1));
+            // (shuffles with the whole wave active: a source lane may be past this round)
+            const uint32_t gstart = __shfl((int)sgl.x, (int)sl, 64), slen = __shfl((int)sgl.y, (int)sl, 64);
+            const uint32_t db = __shfl((int)sgl.z, (int)sl, 64), b = __shfl((int)sgl.w, (int)sl, 64);
+            const uint32_t len = slen * (uint32_t)live;
+            const uint32_t idx = l - pos;
+            uint32_t p = 0, boff = 0, n = 1;
+            uint64_t key = ~0ull;
+            const uint8_t *blk = a.data;
+            if (live) {
+                boff = a.boffs[b];
+                n = a.boffs[b + 1] - boff;
+                blk = a.data + boff;
+                p = a.sa[gstart + idx];
+                key = rot_window(blk, n, p, db);
+            }
+            uint32_t mx = len;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+            uint32_t lt = 0, eqb = 0, eqt = 0;
+            for (uint32_t j = 0; j < mx; ++j) {  // every lane takes part in the shuffles
+                const int src = (int)min(pos + j, 63u);
+                const uint32_t klo = __shfl((uint32_t)key, src, 64), khi = __shfl((uint32_t)(key >> 32), src, 64);
+                const uint64_t kj = ((uint64_t)khi << 32) | klo;
+                const bool m = j < len;
+                lt += m && kj < key;
+                eqt += m && kj == key;
+                eqb += m && kj == key && j < idx;
+            }
+            if (live) {
+                const uint64_t newbits = (uint64_t)db + 64;
+                const bool final_depth = newbits >= 8ull * n;
+                const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
+                if (eqt > 1 && eqb == 0)
+                    dq_push(a, dq, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+                a.sa[slot] = p;
+                if (eqt == 1 || final_depth) {
+                    a.L[slot] = lastcol_byte(blk, n, p);
+                    if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+                }
+            }
+            base = nbase;
         }
     }
     dq_flush<256>(a, dq);
@@ -1613,7 +1642,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             // every pass of a round writes the other buffer of each list
             set_lists(fint_nxt, fin_nxt, finb_nxt, big_nxt);
             if (nfint > 0)
-                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 4 * kTinyPerWave), 256, 0, da, fint_cur, nfint);
+                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 256), 256, 0, da, fint_cur, nfint);
             if (nfin > 0) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
                 BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), nfin, kFinSNT, 0, da, fin_cur, 1u);
                 BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, kFinSCap);
