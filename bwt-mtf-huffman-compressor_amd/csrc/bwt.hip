@@ -851,9 +851,11 @@ struct DTile {
 };
 
 // Bits every rotation of an MSD segment shares below its depth (OR of window XORs against
-// the segment's first rotation); the digit of the pass is taken right after them.
+// the segment's first rotation); the digit of the pass is taken right after them. Each
+// rotation's 64-bit window is kept in kbuf (by slot) so the histogram and scatter passes read it
+// coalesced instead of gathering it from the text again.
 __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                             unsigned long long *__restrict__ segor)
+                                             unsigned long long *__restrict__ segor, uint64_t *__restrict__ kbuf)
 {
     __shared__ uint32_t s_or[2];
     const DTile t = tiles[blockIdx.x];
@@ -864,7 +866,11 @@ __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict_
     __syncthreads();
     const uint64_t w0 = rot_window(blk, n, a.sa[s.x], s.z);
     uint64_t acc = 0;
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) acc |= rot_window(blk, n, a.sa[t.start + e], s.z) ^ w0;
+    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+        const uint64_t w = rot_window(blk, n, a.sa[t.start + e], s.z);
+        kbuf[t.start + e] = w;
+        acc |= w ^ w0;
+    }
     if (acc) {
         atomicOr(&s_or[0], (uint32_t)acc);
         atomicOr(&s_or[1], (uint32_t)(acc >> 32));
@@ -880,8 +886,16 @@ __device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint
     return o ? (uint32_t)__builtin_clzll(o) : 64u;
 }
 
+// the pass digit of slot j: from the stored window, or (digit past the window) from the text
+__device__ __forceinline__ uint32_t msd_digit(const uint64_t *kbuf, uint32_t j, uint32_t cp, const uint8_t *blk, uint32_t n,
+                                              uint32_t p, uint32_t depth)
+{
+    return cp <= 56 ? (uint32_t)((kbuf[j] << cp) >> 56) : (uint32_t)(rot_window(blk, n, p, depth + cp) >> 56);
+}
+
 __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                               const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist)
+                                               const unsigned long long *__restrict__ segor,
+                                               const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
 {
     __shared__ uint32_t h[256];
     const DTile t = tiles[blockIdx.x];
@@ -894,8 +908,10 @@ __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restric
     if (cp == 64) {
         if (threadIdx.x == 0) h[0] = t.len;
     } else {
-        for (uint32_t e = threadIdx.x; e < t.len; e += 256)
-            atomicAdd(&h[(uint32_t)(rot_window(blk, n, a.sa[t.start + e], s.z + cp) >> 56)], 1u);
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+            const uint32_t j = t.start + e;
+            atomicAdd(&h[msd_digit(kbuf, j, cp, blk, n, cp <= 56 ? 0u : a.sa[j], s.z)], 1u);
+        }
     }
     __syncthreads();
     thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
@@ -954,8 +970,9 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
 
 __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
                                                   const unsigned long long *__restrict__ segor,
-                                                  const uint32_t *__restrict__ nomove, const uint32_t *__restrict__ thist,
-                                                  const uint32_t *__restrict__ stot, uint32_t *__restrict__ sa2)
+                                                  const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
+                                                  const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
+                                                  uint32_t *__restrict__ sa2)
 {
     __shared__ uint32_t cur[256];
     const DTile t = tiles[blockIdx.x];
@@ -969,7 +986,7 @@ __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__rest
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
         const uint32_t j = t.start + e;
         const uint32_t p = a.sa[j];
-        const uint32_t d = (uint32_t)(rot_window(blk, n, p, s.z + cp) >> 56);
+        const uint32_t d = msd_digit(kbuf, j, cp, blk, n, p, s.z);
         const uint32_t slot = atomicAdd(&cur[d], 1u);
         sa2[slot] = p;
         if (stot[(size_t)t.seg * 256 + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
@@ -1666,11 +1683,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
                 unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 8 + 64);
                 BMH_HIP(hipMemsetAsync(segor, 0, (size_t)nbig * 8, c->stream));
-                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, thist);
+                // the global-pass records are no longer read: their buffer holds the windows
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor, rec);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, rec, thist);
                 BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, segor, thist, stot, d_nomove);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, d_nomove, thist, stot,
-                           sa2);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, rec, d_nomove, thist,
+                           stot, sa2);
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
             }
             read_counters();
