@@ -754,7 +754,12 @@ __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__re
                     s_pos[i1] = p0;
                 }
             }
-            __syncthreads();
+            // Pairs at distance <= 64 stay inside the 128-slot tile of their q / 64, and every q
+            // of a tile belongs to one wave (q = t + r * NT), so two such stages in a row need
+            // only the wave's own ordering; a wider stage, and the last one, take the barrier.
+            const uint32_t nj = j > 1 ? j >> 1 : k;  // the next stage's distance
+            if (j <= 64 && nj <= 64 && !(k == M && j == 1)) wave_sync();
+            else __syncthreads();
         }
     }
     // runs of equal windows: tails marked in a bitset, each head finds its tail

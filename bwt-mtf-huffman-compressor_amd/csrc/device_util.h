@@ -16,6 +16,16 @@ __device__ __forceinline__ uint32_t writelane(uint32_t val, uint32_t lane, uint3
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
 
+// Ordering point for LDS data that only the calling wave reads and writes: a wave's LDS
+// operations execute in order, so no barrier is needed, only that the compiler keeps the
+// accesses on their side of this point.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One slot of a global list for every active lane, with ONE atomic per wave: callers in
 // divergent code get consecutive indices (single-lane atomics on a shared counter serialise
 // at the L2 when thousands of waves append).
