@@ -182,7 +182,11 @@ __device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q
         q.e[i] = sg;
         q.tag[i] = (l << 24) | atomicAdd(&q.cnt[l], 1u);
     } else {
-        list_base(a, l)[wave_append(list_counter(a, l))] = sg;
+        // lanes of one wave may overflow into different lists: one aggregated append per list,
+        // each under its own branch so that the wave's active lanes share the counter
+#pragma unroll
+        for (uint32_t k = 0; k < kNumLists; ++k)
+            if (l == k) list_base(a, k)[wave_append(list_counter(a, k))] = sg;
     }
 }
 
@@ -1658,11 +1662,46 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 census("fin", fin_cur, nfin);
                 census("finb", finb_cur, nfinb);
                 census("big", big_cur, nbig);
+                // the round's segments must be disjoint
+                std::vector<std::pair<Seg4, int>> all;
+                const Seg4 *lp[4] = {fint_cur, fin_cur, finb_cur, big_cur};
+                const uint32_t lc[4] = {nfint, nfin, nfinb, nbig};
+                for (int li = 0; li < 4; ++li) {
+                    std::vector<Seg4> h(lc[li]);
+                    c->d2h(h.data(), lp[li], lc[li] * sizeof(Seg4));
+                    c->sync();
+                    uint32_t nff = 0;
+                    for (auto &e : h) {
+                        if (e.x == 0xffffffffu) ++nff;
+                        else all.push_back({e, li});
+                    }
+                    if (nff) fprintf(stderr, "  list %d: %u unwritten entries of %u\n", li, nff, lc[li]);
+                }
+                std::sort(all.begin(), all.end(), [](auto &x, auto &y) { return x.first.x < y.first.x; });
+                int nov = 0;
+                static std::vector<std::pair<Seg4, int>> prev;
+                for (size_t i = 1; i < all.size(); ++i)
+                    if (all[i - 1].first.x + all[i - 1].first.y > all[i].first.x && nov++ < 5) {
+                        fprintf(stderr, "  overlap: list %d [%u,+%u) depth %u / list %d [%u,+%u) depth %u\n",
+                                all[i - 1].second, all[i - 1].first.x, all[i - 1].first.y, all[i - 1].first.z,
+                                all[i].second, all[i].first.x, all[i].first.y, all[i].first.z);
+                        const uint32_t x0 = all[i - 1].first.x, x1 = x0 + all[i - 1].first.y;
+                        for (auto &e : prev)
+                            if (e.first.x < x1 && e.first.x + e.first.y > x0)
+                                fprintf(stderr, "    prev round: list %d [%u,+%u) depth %u blk %u\n", e.second, e.first.x,
+                                        e.first.y, e.first.z, e.first.w);
+                    }
+                if (nov) fprintf(stderr, "  %d overlaps\n", nov);
+                prev = all;
             }
             ++round;
             BMH_HIP(hipMemsetAsync(&d_cnt->lcnt[0], 0, 16, c->stream));  // the four per-round lists
             // every pass of a round writes the other buffer of each list
             set_lists(fint_nxt, fin_nxt, finb_nxt, big_nxt);
+            if (dbg_lists) {  // unwritten reserved slots show as all-ones entries
+                BMH_HIP(hipMemsetAsync(fint_nxt, 0xff, seg_cap * 16, c->stream));
+                BMH_HIP(hipMemsetAsync(fin_nxt, 0xff, (N / (kTinyFin + 1) + 2) * 16, c->stream));
+            }
             if (nfint > 0)
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 256), 256, 0, da, fint_cur, nfint);
             if (nfin > 0) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest

@@ -28,7 +28,7 @@ __device__ __forceinline__ void wave_sync()
 
 // One slot of a global list for every active lane, with ONE atomic per wave: callers in
 // divergent code get consecutive indices (single-lane atomics on a shared counter serialise
-// at the L2 when thousands of waves append).
+// at the L2 when thousands of waves append). `ctr` must be the same for every active lane.
 __device__ __forceinline__ uint32_t wave_append(uint32_t *ctr)
 {
     const uint64_t act = __ballot(1);

@@ -78,11 +78,11 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
                 if ((uint32_t)q == (k >> 2)) sw[q] |= x;
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
 #pragma unroll
     for (uint32_t k = 0; k < 64; ++k)
         if (k < nv) atomicMax(&lastpos[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     uint32_t d = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
         if (lp >= 0) atomicOr(&bset[w][lp >> 5], 1u << (lp & 31));
         d += lp >= 0;
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     d = wave_sum(d);
     const uint64_t v = ((uint64_t)bset[w][2 * l + 1] << 32) | bset[w][2 * l];
     const uint32_t cnt = (uint32_t)__builtin_popcountll(v);
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
 #pragma unroll
     for (int k = 0; k < 4; ++k) h[w][4 * l + k] = 0;
     if (s0 < ch.len) {
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
         const uint32_t len = min(kPackChunkSyms, ch.len - s0), a = ch.start + s0, e0 = 64 * l;
         if (len == kPackChunkSyms && ((a + e0) & 15u) == 0) {
             uint32_t sw[16];
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
         } else {
             for (uint32_t k = 0; k < 64 && e0 + k < len; ++k) atomicAdd(&h[w][in[a + e0 + k]], 1u);
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
         uint16_t *co = chist + (size_t)(pfirst[ch.block] + (ch.rel + s0) / kPackChunkSyms) * 256;
 #pragma unroll
         for (int k = 0; k < 4; ++k) co[4 * l + k] = (uint16_t)h[w][4 * l + k];
