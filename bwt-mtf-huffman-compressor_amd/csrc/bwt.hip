@@ -49,6 +49,10 @@ constexpr uint32_t kDataMaxBits = 512;          // deeper MSD ties go to rank do
 constexpr uint32_t kFinMaxBits = 512;           // deeper finish-pass ties go to rank doubling
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
 constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries per workgroup
+#ifndef BMH_TINY_Q
+#define BMH_TINY_Q 256
+#endif
+constexpr uint32_t kTinyQ = BMH_TINY_Q;        // the packed tiny finish (256 segments per workgroup)
 // doubling phase
 constexpr uint32_t kTinyMax = 128;
 constexpr uint32_t kTileT = 1024;
@@ -183,8 +187,9 @@ __device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q
         q.tag[i] = (l << 24) | atomicAdd(&q.cnt[l], 1u);
     } else {
         // lanes of one wave may overflow into different lists: one aggregated append per list,
-        // each under its own branch so that the wave's active lanes share the counter
-#pragma unroll
+        // each under its own branch so that the wave's active lanes share the counter (kept
+        // rolled: the overflow is rare and every push site inlines it)
+#pragma unroll 1
         for (uint32_t k = 0; k < kNumLists; ++k)
             if (l == k) list_base(a, k)[wave_append(list_counter(a, k))] = sg;
     }
@@ -581,7 +586,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 // per segment would leave most lanes idle.
 __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list, uint32_t nlist)
 {
-    __shared__ DeferQueue<kDeferQ> dq;
+    __shared__ DeferQueue<kTinyQ> dq;
     dq_init(dq);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
