@@ -262,6 +262,40 @@ __device__ __forceinline__ uint32_t g1_digit(const uint32_t (&dg)[4], uint32_t k
     return (byte_of(dg, k) << (kG1Bits - 8)) | (b1 >> (16 - kG1Bits));
 }
 
+// Phase timing (experiment builds only): -DBMH_PROF_SCATTER times k_g1_scatter's phases,
+// -DBMH_PROF_DENSE k_finish_dense's; thread 0 of each workgroup stores its s_memtime ticks per
+// phase, and the host prints the means after the dense finish.
+#if defined(BMH_PROF_SCATTER) || defined(BMH_PROF_DENSE)
+__device__ uint32_t g_dprof[(1u << 18) * 8];
+#define PROF_MARK(i)                                                                            \
+    do {                                                                                        \
+        if (threadIdx.x == 0) {                                                                 \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                                   \
+            if (blockIdx.x < (1u << 18)) g_dprof[blockIdx.x * 8 + (i)] = (uint32_t)(_t - _t0); \
+            _t0 = _t;                                                                           \
+        }                                                                                       \
+    } while (0)
+#define PROF_START uint64_t _t0 = __builtin_amdgcn_s_memtime()
+#endif
+#ifdef BMH_PROF_SCATTER
+#define GPROF(i) PROF_MARK(i)
+#define GPROF_START PROF_START
+#else
+#define GPROF(i) \
+    do {         \
+    } while (0)
+#define GPROF_START
+#endif
+#ifdef BMH_PROF_DENSE
+#define DPROF(i) PROF_MARK(i)
+#define DPROF_START PROF_START
+#else
+#define DPROF(i) \
+    do {         \
+    } while (0)
+#define DPROF_START
+#endif
+
 // grid = chunk list; 1024 threads x 16 positions.
 __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
@@ -343,53 +377,70 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
                                                      uint64_t *__restrict__ rec)
 {
     __shared__ uint16_t s_ent[kG1Chunk + 1];  // chunk-relative position (+ a dummy slot)
-    // byte j <-> block position start - 4 + j (cyclic), j < len + 12
-    __shared__ uint32_t s_txt[(kG1Chunk + 12) / 4 + 1];
+    // byte j <-> block position start - 16 + j (cyclic), j < len + 32 (16-byte pieces)
+    __shared__ __align__(16) uint32_t s_txt[(kG1Chunk + 32) / 4];
     __shared__ uint32_t s_cnt[kG1Bins + 1], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
     // (s_cnt[kG1Bins]: sink digit of the slots past the chunk, so the LDS phases run unbranched)
     __shared__ uint32_t s_tmp[17];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
+    GPROF_START;
     const uint32_t t = threadIdx.x;
     const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    for (uint32_t d = t; d < kG1Bins; d += 1024) {
-        s_cnt[d] = 0;
-        s_off[d] = chist[(size_t)blockIdx.x * kG1Bins + d];
-        s_blen[d] = bk[(size_t)b * kG1Bins + d].y;
-    }
+    static_assert(kG1Bins == 1024, "one digit per thread");
+    // the chunk's digit offsets and bucket sizes: loads issued together with the text's
+    const uint32_t cv = chist[(size_t)blockIdx.x * kG1Bins + t], bl = bk[(size_t)b * kG1Bins + t].y;
     {
-        const uint32_t nw = (ch.len + 12 + 3) / 4;
-        for (uint32_t w = t; w < nw; w += 1024) {
-            const int64_t q = (int64_t)ch.start - 4 + 4 * (int64_t)w;
-            const uint8_t *g = blk + q;
-            uint32_t v;
-            if (q >= 0 && q + 4 <= (int64_t)n && (((uintptr_t)g) & 3u) == 0) {
-                v = *(const uint32_t *)g;
-            } else {
-                v = 0;
-                for (int k = 0; k < 4; ++k) {
+        // 16-byte pieces, all loads in flight before the first LDS store (a load under a
+        // per-piece branch waits inside it: one HBM round trip per piece); pieces that wrap
+        // around the block or are unaligned take the byte path
+        const uint32_t np = (ch.len + 26 + 15) / 16;  // bytes up to len + 25 are read
+        constexpr uint32_t PPT = (kG1Chunk + 26 + 15) / 16 / 1024 + 1;  // pieces per thread
+        uint4 v[PPT];
+        bool fast[PPT];
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j) {
+            const uint32_t pc = t + 1024 * j;
+            const int64_t q = (int64_t)ch.start - 16 + 16 * (int64_t)pc;
+            fast[j] = pc < np && q >= 0 && q + 16 <= (int64_t)n && (((uintptr_t)(blk + q)) & 15u) == 0;
+            v[j] = fast[j] ? *(const uint4 *)(blk + q) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < PPT; ++j) {
+            const uint32_t pc = t + 1024 * j;
+            if (pc >= np) continue;
+            if (!fast[j]) {
+                uint32_t u[4] = {0, 0, 0, 0};
+                const int64_t q = (int64_t)ch.start - 16 + 16 * (int64_t)pc;
+                for (int k = 0; k < 16; ++k) {
                     int64_t r = (q + k) % (int64_t)n;
                     if (r < 0) r += n;
-                    v |= (uint32_t)blk[r] << (8 * k);
+                    u[k >> 2] |= (uint32_t)blk[r] << (8 * (k & 3));
                 }
+                v[j] = make_uint4(u[0], u[1], u[2], u[3]);
             }
-            s_txt[w] = v;
+            *(uint4 *)&s_txt[4 * pc] = v[j];
         }
     }
+    s_cnt[t] = 0;
+    s_off[t] = cv;
+    s_blen[t] = bl;
+    GPROF(5);
     __syncthreads();
+    GPROF(0);
     const uint32_t e0 = 16 * t;
     uint32_t dg[4] = {0, 0, 0, 0}, nx = 0;
     const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
     if (nv) {
-        // bytes e0 .. e0 + 16 of the chunk = s_txt bytes e0 + 4 .. e0 + 20 (dword aligned)
-        for (int k = 0; k < 4; ++k) dg[k] = s_txt[(e0 >> 2) + 1 + k];
+        // bytes e0 .. e0 + 16 of the chunk = s_txt bytes e0 + 16 .. e0 + 32 (dword aligned)
+        for (int k = 0; k < 4; ++k) dg[k] = s_txt[(e0 >> 2) + 4 + k];
         if (nv < 16) {
-            const uint32_t j = e0 + 4 + nv;
+            const uint32_t j = e0 + 16 + nv;
             nx = (s_txt[j >> 2] >> (8 * (j & 3u))) & 255u;
             for (uint32_t k = nv; k < 16; ++k) dg[k >> 2] &= ~(255u << (8 * (k & 3)));
         } else {
-            nx = s_txt[(e0 >> 2) + 5] & 255u;
+            nx = s_txt[(e0 >> 2) + 8] & 255u;
         }
     }
     uint32_t dgt[16];
@@ -398,13 +449,14 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) atomicAdd(&s_cnt[dgt[k]], 1u);
     __syncthreads();
+    GPROF(1);
     {
-        static_assert(kG1Bins == 1024, "one digit per thread");
         const uint32_t ex = block_excl_sum<1024>(s_cnt[t], s_tmp, nullptr);
         s_off[t] -= ex;  // slot of local element i with digit d = s_off[d] + i
         s_cnt[t] = ex;
     }
     __syncthreads();
+    GPROF(2);
     {
         uint32_t dst[16];  // all 16 slot reservations in flight before the first wait
 #pragma unroll
@@ -413,12 +465,13 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         for (uint32_t k = 0; k < 16; ++k) s_ent[dgt[k] < kG1Bins ? dst[k] : kG1Chunk] = (uint16_t)(e0 + k);
     }
     __syncthreads();
+    GPROF(3);
 #pragma unroll 4
     for (uint32_t i = t; i < ch.len; i += 1024) {
         const uint32_t rel = s_ent[i];
         const uint32_t p = ch.start + rel;
-        // s_txt bytes rel + 3 .. rel + 11: L byte, byte p, bytes p + 1 .. p + 7
-        const uint32_t j0 = rel + 3, w0 = j0 >> 2, al = (j0 & 3u) * 8u;
+        // s_txt bytes rel + 15 .. rel + 23: L byte, byte p, bytes p + 1 .. p + 7
+        const uint32_t j0 = rel + 15, w0 = j0 >> 2, al = (j0 & 3u) * 8u;
         const uint32_t d0 = s_txt[w0], d1 = s_txt[w0 + 1], d2 = s_txt[w0 + 2];
         const uint64_t lo = ((uint64_t)d1 << 32) | d0;
         const uint64_t v64 = al ? ((lo >> al) | ((uint64_t)d2 << (64 - al))) : lo;  // bytes j0 .. j0 + 7
@@ -438,6 +491,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
             if (p == 0) a.prim[b] = slot;
         }
     }
+    GPROF(7);
 }
 
 // ------------------------------------------------------------------------- finish pass
@@ -473,10 +527,12 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
     const uint32_t t = threadIdx.x;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
+    DPROF_START;
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k)
         if (t + k * NT < len) atomicAdd(&s_cnt[dd[k] >> 1], 1u << (16 * (dd[k] & 1u)));
     __syncthreads();
+    DPROF(1);
     {
         // thread t owns counter words WPT*t .. WPT*t + WPT - 1: counts -> starts
         uint32_t c[2 * WPT], sum = 0;
@@ -494,6 +550,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         }
     }
     __syncthreads();
+    DPROF(2);
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         if (t + k * NT < len) {
@@ -504,6 +561,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         }
     }
     __syncthreads();
+    DPROF(3);
     // s_cnt now holds every sub-bucket's end; its start is the previous digit's end. Rank in
     // registers; outputs are parked in LDS at their segment slot and stored in slot order.
     const uint64_t newbits = (uint64_t)db + kSegDigit + R;
@@ -553,7 +611,9 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         dd[k] = local;  // dd now holds the element's slot in the segment
         if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = gs - boff;
     }
+    DPROF(4);
     dq_flush<NT>(a, dq);
+    DPROF(5);
     // slot -> position (<< 8 | L); a slot whose rotation is not final yet gets its L
     // rewritten when a later pass resolves it
 #pragma unroll
@@ -561,6 +621,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         if (t + k * NT < len) s_rest[dd[k]] = pl[k];
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     __syncthreads();
+    DPROF(6);
     // the SA of a segment nothing defers is never read again (unless rank doubling needs it)
     const bool wsa = a.full_sa || s_tmp[NT / 64 + 1] != 0;
     if (packL) {
@@ -577,6 +638,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         }
     }
     __syncthreads();
+    DPROF(7);
 }
 
 // Tiny list segments (len <= kTinyFin), packed: each wave takes 64 consecutive list entries
@@ -836,6 +898,7 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     const uint2 e = bk[(size_t)b * kG1Bins + (kb & (kG1Bins - 1))];
     if (e.y < 2 || e.y > CAP) return;
     const uint32_t t = threadIdx.x;
+    DPROF_START;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint32_t P = rec_pbits(n), R = rec_rbits(P);
     const bool packL = P <= 24;
@@ -844,10 +907,15 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     dq_init(dq);
     const uint64_t *r0 = rec + boff + e.x;
     uint32_t pl[IPT], dd[IPT], rv[IPT];
+    // every record load in flight before the first is decoded (a load under a per-element
+    // branch waits for its data inside the branch: IPT HBM round trips in a row)
+    uint64_t raw[IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) raw[k] = r0[min(t + k * NT, e.y - 1)];
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
         if (t + k * NT < e.y) {
-            const uint64_t r = r0[t + k * NT];
+            const uint64_t r = raw[k];
             const uint64_t sub = r >> (P + 8);
             const uint32_t p = (uint32_t)(r >> 8) & (uint32_t)((1ull << P) - 1);
             pl[k] = packL ? (p << 8) | ((uint32_t)r & 255u) : p;
@@ -856,6 +924,7 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
         }
     }
     __syncthreads();
+    DPROF(0);
     finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
@@ -1637,6 +1706,22 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         set_lists(fint_cur, fin_cur, finb_cur, big2);
         BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
                    da, bk, rec);
+#if defined(BMH_PROF_SCATTER) || defined(BMH_PROF_DENSE)
+        {
+            std::vector<uint32_t> h((1u << 18) * 8);
+            BMH_HIP(hipStreamSynchronize(c->stream));
+            BMH_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_dprof), h.size() * 4));
+            unsigned long long sum[8] = {}, cnt = 0;
+            for (size_t w = 0; w < (1u << 18); ++w) {
+                if (!h[w * 8 + 7]) continue;
+                ++cnt;
+                for (int i = 0; i < 8; ++i) sum[i] += h[w * 8 + i];
+            }
+            fprintf(stderr, "phases (mean s_memtime ticks per workgroup, %llu workgroups):", cnt);
+            for (int i = 0; i < 8; ++i) fprintf(stderr, " %.0f", cnt ? (double)sum[i] / cnt : 0.0);
+            fprintf(stderr, "\n");
+        }
+#endif
         read_counters();
         uint32_t nfin = h_cnt->lcnt[kListFin], nfint = h_cnt->lcnt[kListTiny], nfinb = h_cnt->lcnt[kListFinb];
         uint32_t nbig = h_cnt->big;
