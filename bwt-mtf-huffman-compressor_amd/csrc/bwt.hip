@@ -566,13 +566,24 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
     // registers; outputs are parked in LDS at their segment slot and stored in slot order.
     const uint64_t newbits = (uint64_t)db + kSegDigit + R;
     const bool final_depth = newbits >= 8ull * n;
+    // the next element's counter words are read before this element's ranking (one LDS round
+    // trip of latency hidden per element)
+    auto bound_words = [&](uint32_t k, uint32_t &w0, uint32_t &w1) {
+        const uint32_t d = t + k * NT < len ? dd[k] & (kSegDigits1 - 1) : 0u;
+        w1 = s_cnt[d >> 1];
+        w0 = s_cnt[((d - 1) >> 1) & (FinishShape<NT, CAP>::NDIG / 2 - 1)];
+    };
+    uint32_t nw0, nw1;
+    bound_words(0, nw0, nw1);
 #pragma unroll
     for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t w0 = nw0, w1 = nw1;
+        if (k + 1 < IPT) bound_words(k + 1, nw0, nw1);
         if (t + k * NT >= len) continue;
         const uint32_t d = dd[k] & (kSegDigits1 - 1), me = dd[k] >> kSegDigit;
         const uint32_t p = packL ? pl[k] >> 8 : pl[k];
-        const uint32_t s1 = (s_cnt[d >> 1] >> (16 * (d & 1u))) & 0xffffu;
-        const uint32_t s0 = d ? (s_cnt[(d - 1) >> 1] >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
+        const uint32_t s1 = (w1 >> (16 * (d & 1u))) & 0xffffu;
+        const uint32_t s0 = d ? (w0 >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
         const uint32_t m = s1 - s0;
         if (m > kSmallM) {
             dd[k] = me;  // deferred, grouped by the 12-bit digit
@@ -590,8 +601,19 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         if (m > 1) {
             const uint64_t key = ((uint64_t)r << 32) | me;
             eqt = 0;
+            // the first four members read together (one LDS round trip; m <= 4 for ~99 % of
+            // the sub-buckets on random data), the rest one by one
+            uint32_t rf4[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) rf4[j] = s_rest[min(s0 + j, s1 - 1)];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const bool in = s0 + j < s1;
+                c += in && ((((uint64_t)rf4[j]) << 32) | (s0 + j)) < key;
+                eqt += in && rf4[j] == r;
+            }
 #pragma nounroll
-            for (uint32_t f = s0; f < s1; ++f) {
+            for (uint32_t f = s0 + 4; f < s1; ++f) {
                 const uint32_t rf = s_rest[f];
                 c += ((((uint64_t)rf) << 32) | f) < key;
                 eqt += rf == r;

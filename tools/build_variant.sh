@@ -10,8 +10,10 @@ make -s -C "$pkg" >/dev/null
 out=$root/variants/$name
 mkdir -p "$out"
 base=$(basename "$src")
+# <src> is a csrc/ file name, or a path to another version of one (e.g. from git show)
+[ -f "$src" ] && srcpath=$src || srcpath=$pkg/csrc/$base
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I"$root/include" --offload-arch=gfx950 \
-    "$@" -c "$pkg/csrc/$base" -o "$out/$base.o"
+    "$@" -I"$pkg/csrc" -c "$srcpath" -o "$out/$base.o"
 objs=""
 for o in "$pkg"/build/*.o; do
     [ "$(basename "$o")" = "$base.o" ] && objs="$objs $out/$base.o" || objs="$objs $o"
