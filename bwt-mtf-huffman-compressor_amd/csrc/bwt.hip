@@ -451,7 +451,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     __syncthreads();
     GPROF(1);
     {
-        const uint32_t ex = block_excl_sum<1024>(s_cnt[t], s_tmp, nullptr);
+        const uint32_t ex = block_excl_sum1<1024>(s_cnt[t], s_tmp);
         s_off[t] -= ex;  // slot of local element i with digit d = s_off[d] + i
         s_cnt[t] = ex;
     }
@@ -542,7 +542,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
             c[2 * j + 1] = w >> 16;
             sum += c[2 * j] + c[2 * j + 1];
         }
-        uint32_t ex = block_excl_sum<NT>(sum, s_tmp, nullptr);
+        uint32_t ex = block_excl_sum1<NT>(sum, s_tmp);
         for (uint32_t j = 0; j < WPT; ++j) {
             const uint32_t e0 = ex, e1 = ex + c[2 * j];
             s_cnt[WPT * t + j] = e0 | (e1 << 16);

@@ -97,6 +97,42 @@ __device__ __forceinline__ uint32_t wave_incl_min_rev(uint32_t x)  // suffix min
 }
 
 // Workgroup exclusive sum of one value per thread. s_tmp needs NT/64 + 1 words.
+// Inclusive wave64 sum by DPP (row shifts inside each 16-lane row, then the row broadcasts
+// of lanes 15 and 31): six VALU steps instead of six dependent ds_bpermute round trips. Every
+// lane of the wave must be active.
+__device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x)
+{
+    // update_dpp(old, src, ctrl, row_mask, bank_mask, bound_ctrl): lanes whose source is out of
+    // the row, and rows outside row_mask, get `old` = 0
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// Workgroup exclusive sum with ONE barrier: each wave publishes its total, then every wave adds
+// the totals of the waves below it (broadcast LDS reads). The caller must pass a barrier before
+// s_tmp[0, NT / 64) is written again. All threads of the workgroup must call it.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_sum1(uint32_t v, uint32_t *s_tmp)
+{
+    constexpr int NW = NT / 64;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t inc = wave_incl_sum_dpp(v);
+    if (lane_id() == 63) s_tmp[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const uint32_t x = s_tmp[j];
+        pre += (uint32_t)j < w ? x : 0u;
+    }
+    return pre + inc - v;
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t *s_tmp, uint32_t *total)
 {
