@@ -33,6 +33,20 @@ namespace bmh {
 namespace {
 
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
+
+// Chunk length used by the host tables (<= kMtfChunk, a multiple of 64; the kernels take any
+// such length). BMH_MTF_CHUNK overrides it for experiments: the encode runs one lane per chunk
+// for ~1 ms, so the number of chunks against the CU slots decides how full its last round is.
+static uint32_t mtf_chunk_len()
+{
+    static const uint32_t v = [] {
+        const char *e = getenv("BMH_MTF_CHUNK");
+        uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 10) : kMtfChunk;
+        x = x < 64 ? 64 : (x > kMtfChunk ? kMtfChunk : x);
+        return x & ~63u;
+    }();
+    return v;
+}
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
 
 struct MChunk {
@@ -515,7 +529,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
             // unaligned prefix) so the encode kernel moves whole 64-byte sectors per lane
             for (uint64_t s = 0; s < n;) {
                 const uint64_t gpos = o + s;
-                const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + kMtfChunk;
+                const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + mtf_chunk_len();
                 const uint64_t e = std::min<uint64_t>(o + n, lim);
                 MChunk m;
                 m.block = b;
