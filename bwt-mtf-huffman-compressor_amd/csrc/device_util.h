@@ -117,19 +117,21 @@ __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x)
 // the totals of the waves below it (broadcast LDS reads). The caller must pass a barrier before
 // s_tmp[0, NT / 64) is written again. All threads of the workgroup must call it.
 template <int NT>
-__device__ __forceinline__ uint32_t block_excl_sum1(uint32_t v, uint32_t *s_tmp)
+__device__ __forceinline__ uint32_t block_excl_sum1(uint32_t v, uint32_t *s_tmp, uint32_t *total = nullptr)
 {
     constexpr int NW = NT / 64;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t inc = wave_incl_sum_dpp(v);
     if (lane_id() == 63) s_tmp[w] = inc;
     __syncthreads();
-    uint32_t pre = 0;
+    uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
         const uint32_t x = s_tmp[j];
         pre += (uint32_t)j < w ? x : 0u;
+        tot += x;
     }
+    if (total) *total = tot;
     return pre + inc - v;
 }
 

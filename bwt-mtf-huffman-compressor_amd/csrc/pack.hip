@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     for (uint32_t k = 0; k < kPackIPT; ++k)
         if (k < nsym) mybits += (uint32_t)s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] & 255u;
     uint32_t total32;
-    const uint32_t tb = block_excl_sum<256>(mybits, s_tmp, &total32) + sh0;  // bit offset from W0 * 32
+    const uint32_t tb = block_excl_sum1<256>(mybits, s_tmp, &total32) + sh0;  // bit offset from W0 * 32
     // the block's last chunk also owns the zero pad bits up to the payload's last byte
     // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
     const bool last = blockIdx.x + 1 == cfirst[ch.block + 1];
