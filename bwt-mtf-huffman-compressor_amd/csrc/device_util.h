@@ -113,6 +113,12 @@ __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x)
     return x;
 }
 
+// Wave64 total by the DPP scan and a read of lane 63 (every lane active).
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum_dpp(x), 63);
+}
+
 // Workgroup exclusive sum with ONE barrier: each wave publishes its total, then every wave adds
 // the totals of the waves below it (broadcast LDS reads). The caller must pass a barrier before
 // s_tmp[0, NT / 64) is written again. All threads of the workgroup must call it.

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     // leaves in first-occurrence order (main.cpp:238-244); first positions are distinct
     uint32_t L = 0;
     for (uint32_t s = lane; s < 256; s += 64) L += s_freq[s] > 0;
-    for (int off = 32; off >= 1; off >>= 1) L += __shfl_xor(L, off, 64);
+    L = wave_sum_dpp(L);
     for (uint32_t s = lane; s < 256; s += 64) s_lkey[s] = s_freq[s] ? s_first[s] : ~0ull;
     __syncthreads();
     {

@@ -105,10 +105,10 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
         d += lp >= 0;
     }
     wave_sync();
-    d = wave_sum(d);
+    d = wave_sum_dpp(d);
     const uint64_t v = ((uint64_t)bset[w][2 * l + 1] << 32) | bset[w][2 * l];
     const uint32_t cnt = (uint32_t)__builtin_popcountll(v);
-    const uint32_t inc = wave_incl_sum(cnt);
+    const uint32_t inc = wave_incl_sum_dpp(cnt);
     uint32_t off = d - inc;  // set bits in lanes above this one
     uint8_t *Rc = R + (size_t)c * 256;
 #pragma unroll
@@ -190,8 +190,8 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
                 cnt += keep[k];
                 kt += keep[k] && 4 * l + k < dt;
             }
-            if (kFinal) dt = d + wave_sum(kt);
-            uint32_t pos = d + wave_incl_sum(cnt) - cnt;
+            if (kFinal) dt = d + wave_sum_dpp(kt);
+            uint32_t pos = d + wave_incl_sum_dpp(cnt) - cnt;
             for (int k = 0; k < 4; ++k)
                 if (keep[k]) s_S[pos++] = (uint8_t)st[k];
             for (uint32_t k = 0; k < 4; ++k)
