@@ -256,3 +256,64 @@ def test_bwt_calgary_batch_repeatable(ctx, oracle):
         L = d_L.download()
         for i, (p, rL) in enumerate(ref):
             assert int(prim[i]) == p and L[int(offs[i]):int(offs[i + 1])].tobytes() == rL, i
+
+
+def _fib_word(n):
+    a, b = b"a", b"ab"
+    while len(b) < n:
+        a, b = b, b + a
+    return b[:n]
+
+
+def _fuzz_blocks(seed, count):
+    """Seeded mixed-structure blocks: log-uniform sizes 1..300 K over uniform, small-alphabet,
+    periodic-with-mutations, Fibonacci-word (deepest tie chains for rank doubling), run-length
+    and Zipf-text generators."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        n = int(np.exp(rng.uniform(0, np.log(300_000)))) or 1
+        kind = i % 6
+        if kind == 0:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            b = rng.integers(0, int(rng.integers(1, 5)), n, dtype=np.uint8).tobytes()
+        elif kind == 2:
+            p = int(rng.integers(1, 64))
+            a = np.resize(rng.integers(0, 256, p, dtype=np.uint8), n)
+            if n > 4:
+                a[rng.integers(0, n, max(1, n // 5000))] ^= 1
+            b = a.tobytes()
+        elif kind == 3:
+            b = _fib_word(n)
+        elif kind == 4:
+            runs = rng.integers(1, 2000, n // 8 + 1)
+            b = np.repeat(rng.integers(0, 4, runs.size, dtype=np.uint8), runs)[:n].tobytes()
+            b = b + bytes(n - len(b))
+        else:
+            b = synth.zipf_text(n).tobytes()
+        out.append(b)
+    return out
+
+
+@pytest.mark.parametrize("seed", [101, 202])
+def test_fuzz_batch_bwt_mtf_roundtrip(ctx, oracle, seed):
+    """One batch of 48 mixed blocks: BWT (L, primary) and MTF bit-exact against the oracle,
+    then encode -> GPU decode restores every block."""
+    blocks = _fuzz_blocks(seed, 48)
+    arrs = [np.frombuffer(b, np.uint8) for b in blocks]
+    offs = np.zeros(len(arrs) + 1, np.uint64)
+    offs[1:] = np.cumsum([a.size for a in arrs])
+    d_in, d_L = ctx.alloc(int(offs[-1])), ctx.alloc(int(offs[-1]))
+    d_in.upload(np.concatenate(arrs))
+    prim = ctx.bwt_dev(d_in, offs, d_L)
+    L = d_L.download()
+    for i, b in enumerate(blocks):
+        op, oL = oracle.bwt(b)
+        got = L[int(offs[i]):int(offs[i + 1])].tobytes()
+        assert int(prim[i]) == op and got == oL, (i, len(b))
+        if i % 4 == 0:
+            assert bmh.move_to_front(b, ctx) == oracle.mtf(b), (i, len(b))
+    recs = ctx.encode_blocks(blocks)
+    for i, (b, r) in enumerate(zip(blocks, recs)):
+        assert ctx.decompress_bytes(r) == b, (i, len(b))
