@@ -317,3 +317,45 @@ def test_fuzz_batch_bwt_mtf_roundtrip(ctx, oracle, seed):
     recs = ctx.encode_blocks(blocks)
     for i, (b, r) in enumerate(zip(blocks, recs)):
         assert ctx.decompress_bytes(r) == b, (i, len(b))
+
+
+@pytest.mark.parametrize("kind", ["random_64m", "zipf_64m", "period5_32m"])
+def test_large_single_block_roundtrip(ctx, kind):
+    """Blocks far past the bench's 4 MiB (the oracle needs over a minute here), checked through
+    size-independent properties: record header n, L a permutation of the block, encode
+    determinism, and encode -> GPU decode restoring the block."""
+    if kind == "random_64m":
+        a = np.random.default_rng(5).integers(0, 256, 64 << 20, dtype=np.uint8)
+    elif kind == "zipf_64m":
+        a = synth.zipf_text(64 << 20)
+    else:
+        a = np.frombuffer((b"abcde" * ((32 << 20) // 5 + 1))[: 32 << 20], np.uint8)
+    data = a.tobytes()
+    d_in, d_L = ctx.alloc(a.size), ctx.alloc(a.size)
+    d_in.upload(a)
+    offs = np.array([0, a.size], np.uint64)
+    prim = ctx.bwt_dev(d_in, offs, d_L)
+    assert 0 <= int(prim[0]) < a.size
+    assert (np.bincount(d_L.download(), minlength=256) == np.bincount(a, minlength=256)).all()
+    r1 = ctx.encode_blocks([data])[0]
+    r2 = ctx.encode_blocks([data])[0]
+    assert r1 == r2
+    assert int(np.frombuffer(r1[:24], np.uint64)[1]) == a.size
+    assert int(np.frombuffer(r1[:24], np.uint64)[0]) == int(prim[0])
+    assert ctx.decompress_bytes(r1) == data
+
+
+def test_device_errors_are_status_codes(ctx):
+    """Empty blocks (the reference segfaults) and short output buffers come back as
+    BMH_EINVAL / BMH_ERANGE, and the context stays usable afterwards."""
+    with pytest.raises(bmh.BmhError) as e:
+        ctx.encode_blocks([b"abc", b""])
+    assert e.value.status == 1  # BMH_EINVAL
+    a = np.random.default_rng(9).integers(0, 256, 1 << 16, dtype=np.uint8)
+    d_in = ctx.alloc(a.size)
+    d_in.upload(a)
+    d_out = ctx.alloc(1024)
+    with pytest.raises(bmh.BmhError) as e:
+        ctx.encode_blocks_dev(d_in, np.array([0, a.size], np.uint64), d_out, 1024)
+    assert e.value.status == 4  # BMH_ERANGE
+    assert ctx.decompress_bytes(ctx.encode_blocks([a.tobytes()])[0]) == a.tobytes()
