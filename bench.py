@@ -124,11 +124,14 @@ def main() -> None:
     ap.add_argument("--decode-steps", type=int, default=3, help="timed GPU decode steps of the same records (0: skip)")
     a = ap.parse_args()
 
-    r = dist.init()
+    # BMH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
+    # the driver's runs use the default (RCCL, one rank per GPU).
+    r = dist.init(os.environ.get("BMH_DIST_BACKEND") or None)
     world = r.world
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    ctx = bmh.Context(r.local_rank)
+    dev = r.local_rank % max(1, int(bmh.lib().bmh_device_count()))
+    ctx = bmh.Context(dev)
 
     bs = a.block_size
     nblk = a.bytes_per_gpu // bs
@@ -150,7 +153,7 @@ def main() -> None:
         try:
             import torch
             if torch.cuda.is_available():
-                torch.cuda.synchronize(r.local_rank)
+                torch.cuda.synchronize(dev)
         except Exception:
             pass
 
