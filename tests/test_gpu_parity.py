@@ -359,3 +359,22 @@ def test_device_errors_are_status_codes(ctx):
         ctx.encode_blocks_dev(d_in, np.array([0, a.size], np.uint64), d_out, 1024)
     assert e.value.status == 4  # BMH_ERANGE
     assert ctx.decompress_bytes(ctx.encode_blocks([a.tobytes()])[0]) == a.tobytes()
+
+
+def test_compress_host_multi_matches_single_context(ctx):
+    """bmh_compress_host_multi (one context + host thread each, blocks dealt round-robin)
+    assembles the same container as one context; here several contexts share the test GPU.
+    Includes more contexts than blocks (a context with nothing to do) and a single block."""
+    data = synth.zipf_text(9_000_007).tobytes()
+    extra = [bmh.Context(0), bmh.Context(0)]
+    try:
+        for bs in (1 << 20, 3 << 20, 1 << 24):  # 9, 3 and 1 blocks
+            single = ctx.compress_bytes(data, block_size=bs)
+            multi = bmh.compress_bytes_multi([ctx] + extra, data, bs)
+            assert multi == single, bs
+            assert ctx.decompress_bytes(multi) == data, bs
+        small = data[:5000]
+        assert bmh.compress_bytes_multi([ctx] + extra, small, 4096) == ctx.compress_bytes(small, block_size=4096)
+    finally:
+        for c in extra:
+            c.close()
