@@ -401,3 +401,32 @@ def test_cli_compress_matches_reference_binary(tmp_path):
         assert r.stdout.endswith(gold[name]), (name, r.stdout)
         r = subprocess.run([cli, "decompress", str(dst), str(back)], capture_output=True, text=True, timeout=60)
         assert r.returncode == 0 and back.read_bytes() == data, name
+
+
+def test_cli_full_pipeline_calgary(tmp_path):
+    """`bmh_full_pipeline <dir>/` (reference main.cpp:416-438): for each of the 14 Calgary files,
+    "k/14 " + the compress line (ending in endl, main.cpp:319-323) + "success"; the .bzap files it leaves equal the reference's
+    records and the .decoded files equal the inputs."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    from oracle_ffi import GOLDEN
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "bwt-mtf-huffman-compressor_amd", "bin", "bmh")
+    d = tmp_path / "calgarycorpus"
+    shutil.copytree(os.path.join(GOLDEN, "calgary"), d)
+    gold = {e["file"]: e["stdout_tail"] for e in json.load(open(os.path.join(GOLDEN, "calgary_stdout.json")))}
+    r = subprocess.run([cli + "_full_pipeline", str(d) + "/"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    names = ["bib", "book1", "book2", "geo", "news", "obj1", "obj2", "paper1", "paper2",
+             "pic", "progc", "progl", "progp", "trans"]
+    assert len(lines) == 28
+    recs = {name: rec for name, _, rec in golden_calgary()}
+    for k, name in enumerate(names, 1):
+        line, verdict = lines[2 * k - 2], lines[2 * k - 1]
+        assert line.startswith(f"{k}/14 ") and line.endswith(gold[name].rstrip("\n")), line
+        assert verdict == "success", (name, verdict)
+        assert (d / (name + ".bzap")).read_bytes() == recs[name], name
+        assert (d / (name + ".decoded")).read_bytes() == (d / name).read_bytes(), name
