@@ -215,7 +215,8 @@ struct DecTable {
     uint16_t child[512][2];           // internal nodes: children (node ids); leaves: 0xffff
     uint8_t sym[512];                 // leaf symbols
     uint32_t single;                  // the root is a leaf: every symbol is sym[0], 0-bit codes
-    uint32_t pad[3];
+    uint32_t maxlen;                  // longest code (tree depth), bits
+    uint32_t pad[2];
 };
 // Parses the preorder tree bytes of a record (bytes_to_tree_dfs, main.cpp:198-219).
 void build_dec_table(const uint8_t *tree, uint64_t tree_len, DecTable *out);

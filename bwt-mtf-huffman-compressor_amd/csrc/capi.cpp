@@ -282,6 +282,9 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
         } catch (const Error &e) {
             st[s] = e.status;
             err[s] = e.what();
+        } catch (const std::bad_alloc &) {
+            st[s] = BMH_ENOMEM;
+            err[s] = "host allocation failed";
         } catch (const std::exception &e) {
             st[s] = BMH_EHIP;
             err[s] = e.what();
@@ -465,6 +468,8 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
                 fn();
             } catch (const Error &e) {
                 fail_all(e.status, e.what());
+            } catch (const std::bad_alloc &) {
+                fail_all(BMH_ENOMEM, "host allocation failed");
             } catch (const std::exception &e) {
                 fail_all(BMH_EHIP, e.what());
             }
@@ -852,6 +857,9 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
         } catch (const Error &e) {
             st[g] = e.status;
             err[g] = e.what();
+        } catch (const std::bad_alloc &) {
+            st[g] = BMH_ENOMEM;
+            err[g] = "host allocation failed";
         } catch (const std::exception &e) {
             st[g] = BMH_EINVAL;
             err[g] = e.what();

@@ -30,6 +30,7 @@ namespace {
 
 constexpr uint32_t kSegBits = 8192;     // Huffman decode segment
 constexpr uint32_t kSyncBnd = 32;       // codeword boundaries recorded per segment
+constexpr int kFixRounds = 4;           // fix-up rounds before the offset-map fallback
 constexpr uint32_t kImtfChunk = 4096;   // inverse-MTF chunk
 constexpr int kImtfLanes = 256;
 constexpr uint32_t kLfChunk = 4096;     // stable-rank chunk (4 waves x 16 x 64 rows)
@@ -234,6 +235,84 @@ __global__ __launch_bounds__(256) void k_hd_fix(const DBlock *__restrict__ blks,
     seg_start[g] = T;
     end_out[g] = pos;
     if (pos != e_old) atomicOr(changed, 1u);
+}
+
+// Fallback when the fix-up rounds do not settle (codes that never resynchronise, e.g. every
+// code word the same length L with kSegBits not a multiple of L): a segment can only be
+// entered at one of maxlen bit offsets past its nominal start (the previous segment's last
+// code word starts before it), so P lanes per segment decode it from every offset o < maxlen
+// and record where each decode leaves the segment and how many symbols it produced:
+// map[g * P + o] = count << 8 | (end - stop). A lane that lands on a boundary of the offset-0
+// decode (pass 1, first kSyncBnd boundaries) takes that decode's remainder.
+__global__ __launch_bounds__(256) void k_hd_map(const DBlock *__restrict__ blks, const DecTable *__restrict__ tabs,
+                                                const uint32_t *__restrict__ seg_block, uint32_t nseg_total, uint32_t P,
+                                                const uint64_t *__restrict__ end0, const uint32_t *__restrict__ cnt0,
+                                                const uint16_t *__restrict__ bnd, uint32_t *__restrict__ map)
+{
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t g = (uint32_t)(t / P), o = (uint32_t)(t % P);
+    if (g >= nseg_total || seg_block[g] == kNil) return;
+    const uint32_t b = seg_block[g];
+    const DBlock B = blks[b];
+    const DecTable *tb = &tabs[b];
+    if (o >= tb->maxlen && o != 0) return;
+    const uint64_t s0 = (uint64_t)(g - B.seg0) * kSegBits;
+    const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
+    if (o == 0) {
+        map[t] = (cnt0[g] << 8) | (uint32_t)(end0[g] - stop);
+        return;
+    }
+    const uint16_t *bb = bnd + (size_t)g * kSyncBnd;
+    uint64_t pos = s0 + o;
+    uint32_t cnt = 0, k = 0;
+    while (pos < stop) {
+        while (k < kSyncBnd && bb[k] != 0xffff && s0 + bb[k] < pos) ++k;
+        if (k < kSyncBnd && bb[k] != 0xffff && s0 + bb[k] == pos) {
+            map[t] = ((cnt + cnt0[g] - k) << 8) | (uint32_t)(end0[g] - stop);
+            return;
+        }
+        uint32_t sym;
+        pos += dec_sym(tb, bits64(B.pay, B.pay_bits, pos), sym);
+        ++cnt;
+    }
+    map[t] = (cnt << 8) | (uint32_t)(pos - stop);
+}
+
+// One wave per block chains the offset maps from the block's first bit: segment g starts at
+// T, produces map[g][T - s0] >> 8 symbols and hands T' = stop + (map & 255) to g + 1. The
+// map rows do not depend on T, so they are loaded kChainAhead segments ahead.
+constexpr uint32_t kChainAhead = 16;
+__global__ __launch_bounds__(64) void k_hd_chain(const DBlock *__restrict__ blks, uint32_t P,
+                                                 const uint32_t *__restrict__ map, uint64_t *__restrict__ seg_start,
+                                                 uint32_t *__restrict__ seg_cnt, uint32_t *status)
+{
+    const DBlock B = blks[blockIdx.x];
+    const uint32_t lane = threadIdx.x;
+    uint64_t T = 0;
+    for (uint32_t k0 = 0; k0 < B.nseg; k0 += kChainAhead) {
+        uint32_t e[kChainAhead];
+#pragma unroll
+        for (uint32_t j = 0; j < kChainAhead; ++j)
+            e[j] = (lane < P && k0 + j < B.nseg) ? map[(size_t)(B.seg0 + k0 + j) * P + lane] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < kChainAhead; ++j) {
+            const uint32_t k = k0 + j;
+            if (k >= B.nseg) break;
+            const uint64_t s0 = (uint64_t)k * kSegBits;
+            const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
+            uint32_t o = (uint32_t)(T - s0);
+            if (o >= P) {  // cannot happen for a well-formed table; keep the walk in range
+                if (lane == 0) atomicOr(status, 1u);
+                o = 0;
+            }
+            const uint32_t v = __shfl(e[j], (int)o, 64);
+            if (lane == 0) {
+                seg_start[B.seg0 + k] = T;
+                seg_cnt[B.seg0 + k] = v >> 8;
+            }
+            T = stop + (v & 255u);
+        }
+    }
 }
 
 // grid = nblocks: exclusive scan of segment counts -> first output symbol of each segment
@@ -846,6 +925,8 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
             fail(BMH_ECORRUPT, "record " + std::to_string(b) + ": bad tree length");
         if (prim >= n) fail(BMH_ECORRUPT, "record " + std::to_string(b) + ": primary index out of range");
         build_dec_table(h + kRecordHeader, tlen, &tabs[b]);
+        // n < 2^32 bounds a Huffman tree's depth far below 64 (Fibonacci growth of the weights)
+        if (tabs[b].maxlen > 64) fail(BMH_ECORRUPT, "record " + std::to_string(b) + ": code longer than 64 bits");
         DBlock &B = hb[b];
         B.pay = d_rec + rec_offs[b] + kRecordHeader + tlen;
         B.pay_bits = (len - kRecordHeader - tlen) * 8;
@@ -911,16 +992,30 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
         for (uint32_t b = 0; b < nb; ++b)
             for (uint32_t k = 0; k < hb[b].nseg; ++k) st0[hb[b].seg0 + k] = (uint64_t)k * kSegBits;
         c->h2d(d_start, st0.data(), nseg * 8);
+        // the offset-0 decode of every segment, kept for the fallback below
+        uint64_t *d_end0 = (uint64_t *)c->get(WS_KEY8, (size_t)nseg * 12 + 64);
+        uint32_t *d_cnt0 = (uint32_t *)(d_end0 + nseg);
+        BMH_HIP(hipMemcpyAsync(d_end0, d_end, (size_t)nseg * 8, hipMemcpyDeviceToDevice, c->stream));
+        BMH_HIP(hipMemcpyAsync(d_cnt0, d_cnt, (size_t)nseg * 4, hipMemcpyDeviceToDevice, c->stream));
         uint32_t *d_changed = d_status + 1;
         uint32_t h_changed = 1;
-        for (int round = 0; h_changed; ++round) {
-            if (round > 64) fail(BMH_ECORRUPT, "decode: Huffman segments do not synchronise");
+        for (int round = 0; h_changed && round < kFixRounds; ++round) {
             BMH_HIP(hipMemsetAsync(d_changed, 0, 4, c->stream));
             BMH_LAUNCH(c, "dec_huff_fix", k_hd_fix, cdiv(nseg, 256), 256, 0, d_blk, d_tab, d_seg_block, nseg, d_end,
                        d_end2, d_start, d_cnt, d_bnd, d_changed);
             std::swap(d_end, d_end2);
             c->d2h(&h_changed, d_changed, 4);
             c->sync();
+        }
+        if (h_changed) {
+            // not settled: every entry offset of every segment, then one chained walk per block
+            uint32_t P = 2;
+            for (uint32_t b = 0; b < nb; ++b)
+                while (hb[b].nseg && P < tabs[b].maxlen) P <<= 1;
+            uint32_t *d_map = (uint32_t *)c->get(WS_RKA, (size_t)nseg * P * 4 + 64);
+            BMH_LAUNCH(c, "dec_huff_map", k_hd_map, (uint32_t)cdiv((uint64_t)nseg * P, 256), 256, 0, d_blk, d_tab,
+                       d_seg_block, nseg, P, d_end0, d_cnt0, d_bnd, d_map);
+            BMH_LAUNCH(c, "dec_huff_chain", k_hd_chain, nb, 64, 0, d_blk, P, d_map, d_start, d_cnt, d_status);
         }
         BMH_LAUNCH(c, "dec_huff_scan", k_hd_scan, nb, 256, 0, d_blk, d_cnt);
         BMH_LAUNCH(c, "dec_huff_pass3", k_hd_pass3, cdiv(nseg, 256), 256, 0, d_blk, d_tab, d_seg_block, nseg, d_start,

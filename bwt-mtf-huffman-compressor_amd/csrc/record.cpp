@@ -171,10 +171,24 @@ void build_dec_table(const uint8_t *tree, uint64_t tree_len, DecTable *out)
     while (!st.empty()) {
         const Item it = st.back();
         st.pop_back();
+        if (t.left[it.v] < 0) out->maxlen = std::max(out->maxlen, it.depth);
         if (t.left[it.v] < 0 || it.depth == kDecLutBits) {
             const uint32_t span = 1u << (kDecLutBits - it.depth), first = it.code << (kDecLutBits - it.depth);
             const uint32_t e = t.left[it.v] < 0 ? ((uint32_t)t.sym[it.v] << 8) | it.depth : (uint32_t)it.v << 16;
             for (uint32_t k = 0; k < span; ++k) out->lut[first + k] = e;
+            if (t.left[it.v] < 0) continue;
+            // a subtree below the LUT depth: its deepest leaf bounds the code length
+            std::vector<std::pair<int, uint32_t>> sub{{it.v, it.depth}};
+            while (!sub.empty()) {
+                const auto [v, d] = sub.back();
+                sub.pop_back();
+                if (t.left[v] < 0) {
+                    out->maxlen = std::max(out->maxlen, d);
+                } else {
+                    sub.push_back({t.left[v], d + 1});
+                    sub.push_back({t.right[v], d + 1});
+                }
+            }
             continue;
         }
         st.push_back({t.right[it.v], (it.code << 1) | 1u, it.depth + 1});
@@ -255,7 +269,13 @@ void decompress(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uin
     std::vector<uint64_t> dst(v.nblocks + 1, 0);
     for (uint64_t b = 0; b < v.nblocks; ++b) dst[b + 1] = dst[b] + record_n(in + v.rec_off[b], v.rec_len[b]);
     if (dst[v.nblocks] != v.total) fail(BMH_ECORRUPT, "container: block sizes do not add up");
-    const unsigned nt = std::max(1u, std::min<unsigned>(std::thread::hardware_concurrency(), 16u));
+    // each thread holds ~6 bytes per symbol of its current block: cap the threads so the
+    // concurrent working set stays under ~6 GiB
+    uint64_t max_n = 1;
+    for (uint64_t b = 0; b < v.nblocks; ++b) max_n = std::max(max_n, dst[b + 1] - dst[b]);
+    const uint64_t mem_threads = std::max<uint64_t>(1, (6ull << 30) / (6 * max_n));
+    const unsigned nt = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>({std::thread::hardware_concurrency(), 16u, mem_threads, v.nblocks}));
     std::vector<std::thread> th;
     std::vector<std::string> errs(nt);
     std::vector<bmh_status> sts(nt, BMH_OK);
@@ -269,6 +289,15 @@ void decompress(const uint8_t *in, uint64_t len, uint8_t *out, uint64_t cap, uin
             } catch (const Error &e) {
                 sts[t] = e.status;
                 errs[t] = e.what();
+            } catch (const std::bad_alloc &) {
+                sts[t] = BMH_ENOMEM;
+                errs[t] = "container: host allocation failed while decoding";
+            } catch (const std::exception &e) {
+                sts[t] = BMH_EINVAL;
+                errs[t] = e.what();
+            } catch (...) {
+                sts[t] = BMH_EINVAL;
+                errs[t] = "container: unknown exception while decoding";
             }
         });
     }

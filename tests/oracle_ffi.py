@@ -44,6 +44,7 @@ class Oracle:
         L.orc_decode_to_mtf.argtypes = [u8p, C.c_size_t, u8p, C.c_size_t]
         L.orc_decode_to_mtf.restype = C.c_int64
         L.orc_huffman_build.argtypes = [u8p, u8p, u8p, u8p, u8p, C.c_size_t]
+        L.orc_huffman_build.restype = C.c_int
         self.L = L
 
     @staticmethod
@@ -79,6 +80,19 @@ class Oracle:
         first = np.zeros(256, np.uint64)
         self.L.orc_histogram(a.ctypes.data, a.size, freq.ctypes.data, first.ctypes.data)
         return freq, first
+
+    def huffman_build(self, freq, first):
+        """Code lengths, codes and tree bytes of the reference's tree (main.cpp:245-254)."""
+        f = np.ascontiguousarray(freq, dtype=np.uint64)
+        fi = np.ascontiguousarray(first, dtype=np.uint64)
+        ln = np.zeros(256, np.uint8)
+        code = np.zeros(256, np.uint64)
+        tree = np.zeros(320, np.uint8)
+        r = self.L.orc_huffman_build(f.ctypes.data, fi.ctypes.data, ln.ctypes.data, code.ctypes.data,
+                                     tree.ctypes.data, tree.size)
+        if r < 0:
+            raise ValueError("oracle huffman_build failed")
+        return ln, code, tree[:r].tobytes()
 
     def encode(self, data, faithful: bool = False) -> bytes:
         a = self._a(data)

@@ -99,6 +99,71 @@ def test_mtf_and_histogram_match_oracle(ctx, oracle, name):
     freq, first = ctx.histogram_dev(d, np.array([0, a.size], np.uint64))
     of, ofi = oracle.histogram(data)
     assert (freq[0] == of).all() and (first[0] == ofi).all()
+    # bmh_mtf_dev's own histogram / first-occurrence outputs (of its MTF stream)
+    d_m = ctx.alloc(a.size)
+    mf, mfi = ctx.mtf_dev(d, np.array([0, a.size], np.uint64), d_m)
+    hf, hfi = oracle.histogram(m)
+    assert (mf[0] == hf).all() and (mfi[0] == hfi).all()
+
+
+def test_mtf_dev_histograms_batched(ctx, oracle):
+    """h_freq / h_first of bmh_mtf_dev (the histogram + first-occurrence scan of huffman(),
+    main.cpp:231-244) for a batch of blocks of mixed size and alphabet, against the oracle."""
+    rng = np.random.default_rng(11)
+    blocks = [rng.integers(0, 256, 70_000, dtype=np.uint8), rng.integers(0, 3, 5_000, dtype=np.uint8),
+              np.frombuffer(b"banana", np.uint8), synth.zipf_text(300_000), np.zeros(9_000, np.uint8)]
+    a = np.concatenate(blocks)
+    offs = np.cumsum([0] + [b.size for b in blocks]).astype(np.uint64)
+    d, d_m = ctx.alloc(a.size), ctx.alloc(a.size)
+    d.upload(a)
+    freq, first = ctx.mtf_dev(d, offs, d_m)
+    m = d_m.download()
+    for i, b in enumerate(blocks):
+        om = oracle.mtf(b)
+        assert m[int(offs[i]):int(offs[i + 1])].tobytes() == om, i
+        of, ofi = oracle.histogram(om)
+        assert (freq[i] == of).all() and (first[i] == ofi).all(), i
+
+
+def _fib_stream(nsym: int, seed: int) -> np.ndarray:
+    """Symbols 0..nsym-1 with Fibonacci frequencies 1, 1, 2, 3, 5, ... in random order: the
+    Huffman tree is a chain, so the rarest symbols get codes nsym-1 bits long."""
+    f = [1, 1]
+    while len(f) < nsym:
+        f.append(f[-1] + f[-2])
+    rng = np.random.default_rng(seed)
+    vals = rng.permutation(nsym).astype(np.uint8)  # which byte value gets which frequency
+    return rng.permutation(np.repeat(vals, f[:nsym]))
+
+
+@pytest.mark.parametrize("nsym", [12, 34, 38])
+def test_pack_dev_long_codes(ctx, oracle, nsym):
+    """bmh_histogram_dev + bmh_huffman_build + bmh_pack_dev (encode_with_huffman,
+    main.cpp:158-172) on a stream whose longest codes are nsym-1 bits (33 and 37 bits take the
+    pack's > 32-bit path): code table and tree equal the oracle's, the payload has the
+    reference's length, decodes back to the stream and is zero-padded."""
+    s = _fib_stream(nsym, nsym)
+    d = ctx.alloc(s.size)
+    d.upload(s)
+    offs = np.array([0, s.size], np.uint64)
+    freq, first = ctx.histogram_dev(d, offs)
+    of, ofi = oracle.histogram(s)
+    assert (freq[0] == of).all() and (first[0] == ofi).all()
+    t = bmh.huffman_build(freq[0], first[0])
+    oln, ocode, otree = oracle.huffman_build(of, ofi)
+    ln = np.frombuffer(bytes(t.len), np.uint8)
+    assert (ln == oln).all() and int(ln.max()) == nsym - 1
+    code = np.ctypeslib.as_array(t.code)
+    assert (code[oln > 0] == ocode[oln > 0]).all()
+    assert t.tree_bytes == otree
+    payload, t2 = bmh.huffman(s, ctx)
+    bits = int((freq[0] * ln.astype(np.uint64)).sum())
+    assert len(payload) == max(1, (bits + 7) // 8) == bmh.payload_bytes(t, freq[0])
+    if bits % 8:
+        assert payload[-1] & ((1 << (8 - bits % 8)) - 1) == 0
+    rec = (np.array([0, s.size, len(otree)], np.uint64).tobytes() + otree + payload)
+    assert oracle.decode_to_mtf(rec) == s.tobytes()
+    assert bmh.record_to_mtf(rec) == s.tobytes()
 
 
 def test_mtf_long_block_chunked(ctx, oracle):
@@ -237,6 +302,52 @@ def test_gpu_decode_random_1g_blocks(ctx):
     oo = ctx.decode_blocks_dev(d_rec, ro, d_dec, bs * nb)
     assert (oo == offs).all()
     assert d_dec.download().tobytes() == d_in.download().tobytes()
+
+
+@pytest.mark.parametrize("alpha", [8, 32, 64, 128])
+def test_gpu_decode_equal_length_codes(ctx, alpha):
+    """iid bytes over 0..alpha-1: the MTF stream stays in that range and every code word has
+    the same length (log2 alpha bits), so a segment decoded from a misaligned start never
+    resynchronises. The GPU decode must still restore every block (offset-map fallback),
+    alone and in a batch with ordinary blocks, and agree with the host decoder."""
+    rng = np.random.default_rng(alpha)
+    big = rng.integers(0, alpha, 1 << 20, dtype=np.uint8).tobytes()
+    rec = ctx.encode_blocks([big])[0]
+    ctx.reset_stats()
+    ctx.set_timing(True)
+    try:
+        assert ctx.decompress_bytes(rec) == big
+        assert "dec_huff_map" in ctx.kernel_stats()  # the fix-up rounds alone cannot settle this
+    finally:
+        ctx.set_timing(False)
+    assert bmh.decompress_bytes(rec) == big
+    blocks = [rng.integers(0, alpha, n, dtype=np.uint8).tobytes() for n in (300_001, 77_777, 5)]
+    blocks.insert(1, synth.zipf_text(200_000).tobytes())
+    data = b"".join(blocks)
+    out = ctx.compress_bytes(data, block_size=len(blocks[0]))
+    assert ctx.decompress_bytes(out) == data
+
+
+@pytest.mark.parametrize("mutate", ["truncate", "bad_n", "bad_tree_len", "bad_primary", "short_payload"])
+def test_gpu_decode_corrupt_records(ctx, mutate):
+    """Malformed records (cf. decompress(), main.cpp:327-345, which has no checks) come back
+    from the GPU decoder as BMH_ECORRUPT, and the context decodes a good record afterwards."""
+    name, data, rec = next(golden_calgary())
+    r = bytearray(rec)
+    if mutate == "truncate":
+        r = r[:100]
+    elif mutate == "bad_n":
+        r[8:16] = (10 ** 12).to_bytes(8, "little")
+    elif mutate == "bad_tree_len":
+        r[16:24] = (10 ** 6).to_bytes(8, "little")
+    elif mutate == "bad_primary":
+        r[0:8] = (len(data) + 5).to_bytes(8, "little")
+    else:  # n 10 % larger than the payload holds (passes the header checks): the decode runs dry
+        r[8:16] = (len(data) * 11 // 10).to_bytes(8, "little")
+    with pytest.raises(bmh.BmhError) as e:
+        ctx.decompress_bytes(bytes(r))
+    assert e.value.status == 5, (mutate, e.value)  # BMH_ECORRUPT
+    assert ctx.decompress_bytes(rec) == data
 
 
 @pytest.mark.gpu

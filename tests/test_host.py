@@ -140,3 +140,28 @@ def test_cli_host_modes(tmp_path):
     if bmh.lib().bmh_device_count() == 0:
         r = subprocess.run([CLI, "compress", str(out), str(tmp_path / "x.bzap")], capture_output=True, text=True)
         assert r.returncode != 0 and "device" in (r.stderr + r.stdout).lower()
+
+
+@pytest.mark.parametrize("nsym", [2, 12, 34, 38, 60])
+def test_huffman_build_long_codes_matches_oracle(oracle, nsym):
+    """bmh_huffman_build (host; huffman() tree, main.cpp:245-254) on Fibonacci frequencies,
+    whose tree is a chain with codes up to nsym-1 bits (beyond 32 and up to 59), against the
+    oracle's code lengths, codes and tree bytes, with leaves in a shuffled first-occurrence
+    order."""
+    f = [1, 1]
+    while len(f) < nsym:
+        f.append(f[-1] + f[-2])
+    rng = np.random.default_rng(nsym)
+    vals = rng.permutation(256)[:nsym]
+    freq = np.zeros(256, np.uint64)
+    first = np.full(256, np.iinfo(np.uint64).max, np.uint64)
+    freq[vals] = f[:nsym]
+    first[vals] = rng.permutation(nsym).astype(np.uint64) * 7
+    t = bmh.huffman_build(freq, first)
+    oln, ocode, otree = oracle.huffman_build(freq, first)
+    ln = np.frombuffer(bytes(t.len), np.uint8)
+    assert (ln == oln).all() and int(ln.max()) == nsym - 1
+    code = np.ctypeslib.as_array(t.code)
+    assert (code[oln > 0] == ocode[oln > 0]).all()
+    assert t.tree_bytes == otree
+    assert bmh.payload_bytes(t, freq) == max(1, (int((freq * ln.astype(np.uint64)).sum()) + 7) // 8)
