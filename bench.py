@@ -1,13 +1,26 @@
 #!/usr/bin/env python3
 """Headline benchmark: BWT -> MTF -> Huffman block encode on MI355X.
 
-Metric (BASELINE.json): encode MB/s (and ratio) — workload = BASELINE config 4, 1 GiB of
-uniform-random bytes (splitmix64 seed 0) in 4 MiB blocks per GPU. A "step"
-encodes the rank's whole 1 GiB batch (256 blocks) from HBM to reference records in HBM.
-Weak scaling: rank r owns global blocks r, r+N, r+2N, ... of the N GiB stream (round-robin,
-no collective on the data path); value = bytes of all ranks / max-over-ranks time.
+Metric (BASELINE.json): encode MB/s and ratio on Calgary + 1 GiB synthetic at 1/2/4/8 GPUs.
+Workload (BASELINE config 4): uniform-random bytes (splitmix64 seed 0) in
+4 MiB blocks, dealt round-robin to the ranks (global block b -> rank b mod N, no collective
+on the data path). A "step" encodes the rank's whole batch from HBM to reference records in
+HBM.
+  --scaling weak   (default) 1 GiB per GPU: rank r owns blocks r, r+N, r+2N, ... of the N GiB
+                   stream.
+  --scaling strong 1 GiB in total (256 blocks) dealt over the N GPUs (config 4 as written).
+value = input bytes of all ranks x steps / max-over-ranks time.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+Beside `value` (device-resident, the contract's figure) the line carries:
+  pcie_inclusive  SURVEY §8(d)'s graded t_encode: the same blocks streamed by bmh_compress_host
+                  from page-locked host memory (first H2D) to the records in page-locked host
+                  memory (last D2H), and its graded roofline fraction.
+  calgary         MB/s and ratio on the Calgary corpus: whole files and 256 KiB blocks.
+  roofline        the dominant kernel at SURVEY §8(d)'s 1 algorithmic byte per input byte.
+  cpu_baseline    the reference itself (oracle/_ref/ref_COMPRESS, compiled from its sources)
+                  on every host core of the box, one 4 MiB block per process; plus Calgary.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
   torchrun --nproc-per-node N bench.py --gpus N ...     (one process per GPU)
 
 Prints ONE JSON line on rank 0 (plus diagnostics on stderr).
@@ -15,6 +28,7 @@ Prints ONE JSON line on rank 0 (plus diagnostics on stderr).
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import hashlib
 import json
 import os
@@ -27,6 +41,7 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(REPO, "bwt-mtf-huffman-compressor_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
 sys.path.insert(0, PKG)
 
 import bmh  # noqa: E402
@@ -34,13 +49,13 @@ from bmh import dist, synth  # noqa: E402
 
 METRIC = "encode MB/s and ratio on Calgary + 1 GiB synthetic at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+CALGARY = ["bib", "book1", "book2", "geo", "news", "obj1", "obj2", "paper1", "paper2",
+           "pic", "progc", "progl", "progp", "trans"]
 
-# Algorithmic HBM bytes per input byte of the batch for the kernels that sweep the whole
-# batch once per launch (DESIGN.md §4 states and justifies each figure).
 # roofline.achieved uses SURVEY.md §8(d)'s graded per-unit figure: 1 algorithmic HBM byte per
 # input byte ("HBM-read roofline"), times the input bytes one launch processes. Every kernel
-# below processes the whole batch per launch. STAGE_BYTES_PER_INPUT_BYTE is the
-# diagnostic per-stage traffic model (minimum bytes each kernel must move).
+# below processes the whole batch per launch. STAGE_BYTES_PER_INPUT_BYTE is the diagnostic
+# per-stage traffic model (minimum bytes each kernel must move).
 ALGO_BYTES_PER_INPUT_BYTE = 1.0
 STAGE_BYTES_PER_INPUT_BYTE = {
     "bwt_g1_hist": 1.0,         # read input
@@ -58,70 +73,292 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(block_size: int, nsample: int) -> dict:
-    """The reference CPU path (oracle/_ref/ref_COMPRESS, compiled from the reference sources)
-    on a bounded sample of the same workload, one process per block, all in parallel."""
-    ref = os.path.join(REPO, "oracle", "_ref", "ref_COMPRESS")
-    tmp = tempfile.mkdtemp(prefix="bmh_cpu_")
-    files = []
-    for b in range(nsample):
-        p = os.path.join(tmp, f"b{b:04d}")
-        synth.splitmix64_bytes(0, b * block_size, block_size).tofile(p)
-        files.append(p)
-    kind = "reference"
-    t0 = time.perf_counter()
-    if os.path.exists(ref):
-        procs = [subprocess.Popen([ref, f, f + ".bzap"], stdout=subprocess.DEVNULL) for f in files]
-        rcs = [p.wait() for p in procs]
-        wall = time.perf_counter() - t0
-        ok = all(rc == 0 for rc in rcs)
-    else:  # the from-scratch C port (oracle.c), one thread per block
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        from concurrent.futures import ThreadPoolExecutor
+# --------------------------------------------------------------------------- plan / legs
+def rank_plan(rank: int, world: int, block_size: int, scaling: str, bytes_per_gpu: int,
+              total_bytes: int) -> list[int]:
+    """Global block ids this rank encodes (block b -> rank b mod world)."""
+    if scaling == "strong":
+        return dist.rank_blocks(total_bytes // block_size, rank, world)
+    return [rank + world * i for i in range(bytes_per_gpu // block_size)]
 
-        from oracle_ffi import Oracle
-        orc = Oracle()
-        kind = "port"
 
-        def one(f):
-            rec = orc.encode(np.fromfile(f, np.uint8), faithful=True)
-            with open(f + ".bzap", "wb") as g:
-                g.write(rec)
-        with ThreadPoolExecutor(nsample) as ex:
-            list(ex.map(one, files))
-        wall = time.perf_counter() - t0
-        ok = True
-    # parity of the baseline itself against the committed manifest
+def encode_leg(r: dist.Rank, enc, steps: int, warmup: int) -> dict:
+    """W untimed + K timed steps of enc.step() between barriers (max over ranks); bytes summed
+    over ranks. `enc` is the rank's encoder: the GPU path here, a CPU stand-in in the gloo
+    tests (tests/test_dist.py) — the sharding / timing code is the same."""
+    dt = dist.timed_steps(r, enc.step, steps, warmup, enc.sync)
+    return {"dt": dt, "in_bytes": dist.sum_over_ranks(r, float(enc.in_bytes)),
+            "out_bytes": dist.sum_over_ranks(r, float(enc.out_bytes()))}
+
+
+def parity_leg(r: dist.Rank, recs: list[bytes], mine: list[int], block_size: int) -> str:
+    """Every record of this rank against the reference manifest (config 4: blocks 0..255 at
+    4 MiB); counts summed over ranks."""
+    if block_size != 1 << 22:
+        return "unchecked (no reference manifest for this block size)"
+    with open(os.path.join(GOLDEN, "manifests", "random_1g_4m.json")) as f:
+        man = json.load(f)["blocks"]
+    ok = chk = 0
+    for rec, b in zip(recs, mine):
+        if b < len(man):
+            chk += 1
+            ok += hashlib.sha256(rec).hexdigest() == man[b]["sha256"]
+    ok = int(dist.sum_over_ranks(r, float(ok)))
+    chk = int(dist.sum_over_ranks(r, float(chk)))
+    return f"{ok}/{chk} records byte-identical to the reference manifest"
+
+
+class DeviceEncoder:
+    """The product path on one GPU: the rank's blocks generated straight into HBM, encoded
+    HBM -> HBM by bmh_encode_blocks_dev (records back to back in HBM)."""
+
+    def __init__(self, ctx: bmh.Context, mine: list[int], bs: int):
+        self.ctx, self.mine, self.bs = ctx, mine, bs
+        nblk = len(mine)
+        self.in_bytes = nblk * bs
+        self.offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
+        self.d_in = ctx.alloc(max(1, self.in_bytes))
+        for i, b in enumerate(mine):
+            ctx.synth_splitmix64(self.d_in.ptr.value + i * bs, bs, 0, b * bs)
+        self.cap = nblk * int(bmh.lib().bmh_record_bound(bs))
+        self.d_out = ctx.alloc(max(1, self.cap))
+        self.ro = np.zeros(nblk + 1, np.uint64)
+
+    def step(self):
+        if self.mine:
+            self.ro = self.ctx.encode_blocks_dev(self.d_in, self.offs, self.d_out, self.cap)
+
+    def sync(self):
+        pass  # every bmh call returns with its work complete (stream-synchronous)
+
+    def out_bytes(self) -> int:
+        return int(self.ro[-1])
+
+    def records(self) -> list[bytes]:
+        if not self.mine:
+            return []
+        a = self.d_out.download(int(self.ro[-1])).tobytes()
+        return [a[int(self.ro[i]):int(self.ro[i + 1])] for i in range(len(self.mine))]
+
+
+def kernel_leg(enc: DeviceEncoder, ksteps: int) -> tuple[dict, dict]:
+    """A separate pass with HIP events around every launch on the context stream. The timed
+    region splits each batch over 2 streams (kernels overlap, stretching their individual
+    durations); this pass runs one stream so each kernel's duration is its own."""
+    ctx = enc.ctx
+    streams_env = os.environ.get("BMH_STREAMS")
+    os.environ["BMH_STREAMS"] = "1"
+    ctx.reset_stats()
+    ctx.set_timing(True)
+    for _ in range(ksteps):
+        enc.step()
+    stats = ctx.kernel_stats()
+    ctx.set_timing(False)
+    if streams_env is None:
+        del os.environ["BMH_STREAMS"]
+    else:
+        os.environ["BMH_STREAMS"] = streams_env
+    walls = {k[5:]: v for k, v in stats.items() if k.startswith("wall:")}
+    stats = {k: v for k, v in stats.items() if not k.startswith("wall:")}
+    return stats, walls
+
+
+def roofline(stats: dict, ksteps: int, batch_bytes: int) -> dict | None:
+    if not stats:
+        return None
+    name, (launches, ms) = max(stats.items(), key=lambda kv: kv[1][1])
+    lps = launches / ksteps
+    avg_s = ms / launches / 1e3
+    per_launch = ALGO_BYTES_PER_INPUT_BYTE * batch_bytes / lps  # batch bytes per launch
+    ach = per_launch / avg_s / 1e9
+    traffic = None
+    try:  # HBM bytes per launch from the committed PMC summary of this workload
+        pm = json.load(open(PMC_TRAFFIC))
+        if pm.get("workload_bytes") == batch_bytes and name in pm.get("kernels", {}):
+            traffic = pm["kernels"][name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
+    stage = STAGE_BYTES_PER_INPUT_BYTE.get(name)
+    return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "measured": "HIP events on the kernel's stream, 1-stream kernel pass of the same workload",
+            "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
+            "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": lps,
+            "algorithmic_bytes_per_launch": per_launch,
+            "stage_model_bytes_per_launch": stage * batch_bytes if stage else None,
+            "stage_model_frac": round(stage * batch_bytes / avg_s / 1e9 / HBM_PEAK_GBS, 4) if stage else None}
+
+
+def pcie_leg(r: dist.Rank, enc: DeviceEncoder, steps: int, warmup: int) -> dict:
+    """SURVEY §8(d) graded t_encode: the rank's blocks in page-locked host memory, streamed by
+    bmh_compress_host (H2D / encode / D2H overlapped on separate streams) until the last record
+    lands in page-locked host memory; checked record for record against the device encode."""
+    ctx, n, bs = enc.ctx, enc.in_bytes, enc.bs
+    lib = bmh.lib()
+    hin = ctx.alloc_host(n)
+    cap = int(lib.bmh_compress_bound(n, bs))
+    hout = ctx.alloc_host(cap)
     try:
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        from oracle_ffi import manifest
-        man = manifest("random_1g_4m")["blocks"] if block_size == 1 << 22 else None
-        if man:
+        if n:
+            bmh._check(lib.bmh_memcpy_d2h(ctx.h, hin.ptr, enc.d_in.ptr, n), "d2h")
+        olen = [0]
+
+        def step():
+            if n:
+                olen[0] = ctx.compress_into(hin.a, bs, hout.a)
+        dt = dist.timed_steps(r, step, steps, warmup, lambda: None)
+        recs = enc.records()
+        if len(recs) > 1:
+            body = hout.a[32 + 8 * len(recs): olen[0]].tobytes()
+        else:
+            body = hout.a[: olen[0]].tobytes()
+        ok = body == b"".join(recs)
+        ok = int(dist.sum_over_ranks(r, float(ok))) == r.world
+    finally:
+        hin.free()
+        hout.free()
+    tot = dist.sum_over_ranks(r, float(n))
+    mbs = tot * steps / dt / 1e6
+    return {"value": round(mbs, 2), "unit": "MB/s", "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+            "timed": "bmh_compress_host, page-locked input -> page-locked output (first H2D .. last record in host "
+                     "memory), every rank at once, max over ranks",
+            "graded_roofline_frac": round(mbs / 1e3 / (r.world * HBM_PEAK_GBS), 6),
+            "records_equal_device_encode": bool(ok),
+            "stream_batch_bytes": int(os.environ.get("BMH_STREAM_BATCH", 256 << 20))}
+
+
+def calgary_leg(ctx: bmh.Context, steps: int) -> dict:
+    """Calgary corpus (BASELINE configs 1-2) encoded on the GPU from HBM: the 14 files as one
+    batch of whole-file blocks, and cut into 256 KiB blocks; records checked against the
+    reference's (golden records / manifest)."""
+    datas = [open(os.path.join(GOLDEN, "calgary", f), "rb").read() for f in CALGARY]
+    gold = [open(os.path.join(GOLDEN, "calgary_records", f + ".bzap"), "rb").read() for f in CALGARY]
+    with open(os.path.join(GOLDEN, "manifests", "calgary_256k.json")) as f:
+        man = json.load(f)
+    out = {}
+    for mode, blocks in (("whole_files", datas),
+                         ("blocks_256k", [d[i:i + (1 << 18)] for d in datas for i in range(0, len(d), 1 << 18)])):
+        a = np.frombuffer(b"".join(blocks), np.uint8)
+        offs = np.cumsum([0] + [len(b) for b in blocks]).astype(np.uint64)
+        d_in = ctx.alloc(a.size)
+        d_in.upload(a)
+        cap = sum(int(bmh.lib().bmh_record_bound(len(b))) for b in blocks)
+        d_out = ctx.alloc(cap)
+        ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+        dt = (time.perf_counter() - t0) / steps
+        recs = d_out.download(int(ro[-1])).tobytes()
+        if mode == "whole_files":
+            exact = recs == b"".join(gold)
+        else:
+            exact = hashlib.sha256(recs).hexdigest() == man["aggregate_sha256"]
+        out[mode] = {"blocks": len(blocks), "bytes": int(a.size), "ms": round(dt * 1e3, 3),
+                     "MBps": round(a.size / dt / 1e6, 2), "ratio": round(int(ro[-1]) / a.size, 6),
+                     "records_byte_identical_to_reference": bool(exact)}
+        d_in.free()
+        d_out.free()
+    return out
+
+
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota,
+            "model": model}
+
+
+def cpu_baseline(block_size: int, procs: int | None) -> dict:
+    """The reference CPU path (oracle/_ref/ref_COMPRESS, compiled from the reference sources
+    by oracle/Makefile) on the box's host cores: one process per 4 MiB block of the same
+    stream, all at once (one block per core), wall clock from first spawn to last exit;
+    records checked against the manifest. Calgary: the 14 files, one process each."""
+    hc = host_cpu()
+    # every core this process may use: the affinity set, capped by the cgroup's CPU quota
+    # (more processes than the quota only time-slice: measured 59 MB/s with 256 processes
+    # under a 16-CPU quota vs 96 MB/s with 16)
+    avail = hc["affinity"]
+    if hc["cgroup_cpu_quota"]:
+        avail = min(avail, max(1, int(hc["cgroup_cpu_quota"])))
+    P = max(1, min(procs or avail, 512))
+    ref = os.path.join(REPO, "oracle", "_ref", "ref_COMPRESS")
+    if not os.path.exists(ref):
+        return {"value": None, "unit": "MB/s", "cores": 0, "kind": "reference",
+                "sample": "oracle/_ref/ref_COMPRESS not built", **hc}
+    tmp = tempfile.mkdtemp(prefix="bmh_cpu_")
+    try:
+        files = []
+        for b in range(P):
+            p = os.path.join(tmp, f"b{b:04d}")
+            synth.splitmix64_bytes(0, b * block_size, block_size).tofile(p)
+            files.append(p)
+
+        def run_all(paths):
+            t0 = time.perf_counter()
+            ps = [subprocess.Popen([ref, f, f + ".bzap"], stdout=subprocess.DEVNULL) for f in paths]
+            rcs = [p.wait() for p in ps]
+            return time.perf_counter() - t0, all(rc == 0 for rc in rcs)
+        wall, ok = run_all(files)
+        if block_size == 1 << 22:
+            with open(os.path.join(GOLDEN, "manifests", "random_1g_4m.json")) as f:
+                man = json.load(f)["blocks"]
             for b, f in enumerate(files):
-                with open(f + ".bzap", "rb") as g:
-                    ok &= hashlib.sha256(g.read()).hexdigest() == man[b]["sha256"]
-    except Exception as e:  # pragma: no cover
-        log("cpu_baseline manifest check skipped:", e)
-    for f in files:
-        for x in (f, f + ".bzap"):
-            if os.path.exists(x):
-                os.remove(x)
-    os.rmdir(tmp)
-    return {"value": round(nsample * block_size / wall / 1e6, 3), "unit": "MB/s", "cores": nsample,
-            "kind": kind, "sample": f"{nsample} x {block_size >> 20} MiB splitmix64 blocks (global blocks "
-            f"0..{nsample - 1}), one process per block, wall {wall:.2f} s, records match manifest: {ok}"}
+                if b < len(man):
+                    with open(f + ".bzap", "rb") as g:
+                        ok &= hashlib.sha256(g.read()).hexdigest() == man[b]["sha256"]
+        cal = []
+        for name in CALGARY:
+            p = os.path.join(tmp, name)
+            with open(os.path.join(GOLDEN, "calgary", name), "rb") as s, open(p, "wb") as d:
+                d.write(s.read())
+            cal.append(p)
+        cwall, cok = run_all(cal)
+        cin = sum(os.path.getsize(p) for p in cal)
+        cout = sum(os.path.getsize(p + ".bzap") for p in cal)
+        for name, p in zip(CALGARY, cal):
+            with open(p + ".bzap", "rb") as a, open(os.path.join(GOLDEN, "calgary_records", name + ".bzap"), "rb") as g:
+                cok &= a.read() == g.read()
+    finally:
+        for f in os.listdir(tmp):
+            os.remove(os.path.join(tmp, f))
+        os.rmdir(tmp)
+    return {"value": round(P * block_size / wall / 1e6, 3), "unit": "MB/s", "cores": P, "kind": "reference",
+            "sample": f"{P} x {block_size >> 20} MiB splitmix64 blocks (global blocks 0..{P - 1}), one ref_COMPRESS "
+                      f"process per block, all at once on the {P} cores available (affinity {hc['affinity']}, "
+                      f"cgroup quota {hc['cgroup_cpu_quota']}); wall {wall:.2f} s; records match manifest: {ok}",
+            "host": hc,
+            "calgary": {"MBps": round(cin / cwall / 1e6, 3), "ratio": round(cout / cin, 6), "wall_s": round(cwall, 3),
+                        "procs": len(cal), "records_match_reference": bool(cok)}}
 
 
+# ------------------------------------------------------------------------------- main
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     ap.add_argument("--block-size", type=int, default=4 << 20)
-    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30, help="weak scaling: bytes per rank")
+    ap.add_argument("--total-bytes", type=int, default=1 << 30, help="strong scaling: bytes over all ranks")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0, help="blocks in the CPU sample (default: host threads, <=16)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="CPU baseline processes (default: all host cores)")
     ap.add_argument("--decode-steps", type=int, default=3, help="timed GPU decode steps of the same records (0: skip)")
+    ap.add_argument("--pcie-steps", type=int, default=3, help="timed host-buffer steps (0: skip)")
+    ap.add_argument("--calgary-steps", type=int, default=10, help="timed Calgary steps (0: skip)")
     a = ap.parse_args()
 
     # BMH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
@@ -132,138 +369,75 @@ def main() -> None:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     dev = r.local_rank % max(1, int(bmh.lib().bmh_device_count()))
     ctx = bmh.Context(dev)
-
     bs = a.block_size
-    nblk = a.bytes_per_gpu // bs
-    mine = [r.rank + world * i for i in range(nblk)]  # global blocks of this rank
-    total = nblk * bs
-    offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
-    d_in = ctx.alloc(total)
-    for i, b in enumerate(mine):  # synthetic input generated straight into HBM
-        ctx.synth_splitmix64(d_in.ptr.value + i * bs, bs, 0, b * bs)
-    cap = int(sum(int(bmh.lib().bmh_record_bound(bs)) for _ in range(nblk)))
-    d_out = ctx.alloc(cap)
-    rec_offs = [None]
+    mine = rank_plan(r.rank, world, bs, a.scaling, a.bytes_per_gpu, a.total_bytes)
+    enc = DeviceEncoder(ctx, mine, bs)
 
-    def step():
-        rec_offs[0] = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
-
-    def sync():
-        # every call is host-synchronous on the context stream; also drain the device
-        try:
-            import torch
-            if torch.cuda.is_available():
-                torch.cuda.synchronize(dev)
-        except Exception:
-            pass
-
-    for _ in range(a.warmup):
-        step()
-    # the timed region runs without per-kernel events ...
-    dt = dist.timed_steps(r, step, a.steps, 0, sync)
-    # ... then a separate pass with HIP events around every launch for the kernel breakdown.
-    # The timed region splits each batch over 2 streams (kernels overlap, which stretches
-    # their individual durations); the per-kernel pass runs one stream so each kernel's
-    # duration (and so its roofline) is its own.
+    res = encode_leg(r, enc, a.steps, a.warmup)
     ksteps = max(1, min(a.steps, 5))
-    streams_env = os.environ.get("BMH_STREAMS")
-    os.environ["BMH_STREAMS"] = "1"
-    ctx.reset_stats()
-    ctx.set_timing(True)
-    for _ in range(ksteps):
-        step()
-    sync()
-    stats = ctx.kernel_stats()
-    ctx.set_timing(False)
-    if streams_env is None:
-        del os.environ["BMH_STREAMS"]
-    else:
-        os.environ["BMH_STREAMS"] = streams_env
-    walls = {k[5:]: v for k, v in stats.items() if k.startswith("wall:")}
-    stats = {k: v for k, v in stats.items() if not k.startswith("wall:")}
+    stats, walls = kernel_leg(enc, ksteps)
+    recs = enc.records()
+    parity = parity_leg(r, recs, mine, bs)
 
-    ro = rec_offs[0]
-    out_bytes = dist.sum_over_ranks(r, float(ro[-1]))
-    # decode of the same records on the same GPU (GPU decode), timed the same way,
-    # with a full round-trip check of this rank's batch; reported beside the encode line
+    # decode of the same records on the same GPU (GPU decode), with a full
+    # round-trip check of this rank's batch; reported beside the encode line
     dec = None
-    if a.decode_steps > 0:
-        d_dec = ctx.alloc(total)
-        ro_host = np.ascontiguousarray(ro, dtype=np.uint64)
+    if a.decode_steps > 0 and mine:
+        d_dec = ctx.alloc(enc.in_bytes)
+        ro_host = np.ascontiguousarray(enc.ro, dtype=np.uint64)
 
-        def dstep():
-            ctx.decode_blocks_dev(d_out, ro_host, d_dec, total)
-        dstep()
-        ddt = dist.timed_steps(r, dstep, a.decode_steps, 0, sync)
-        ok = d_dec.download().tobytes() == d_in.download().tobytes()
+        class _Dec:
+            in_bytes = enc.in_bytes
+
+            @staticmethod
+            def step():
+                ctx.decode_blocks_dev(enc.d_out, ro_host, d_dec, enc.in_bytes)
+
+            @staticmethod
+            def sync():
+                pass
+
+            @staticmethod
+            def out_bytes():
+                return enc.in_bytes
+        dres = encode_leg(r, _Dec, a.decode_steps, 1)
+        ok = d_dec.download().tobytes() == enc.d_in.download().tobytes()
         ok = dist.sum_over_ranks(r, float(ok)) == world
-        dec = {"value": round(float(total) * world * a.decode_steps / ddt / 1e6, 2), "unit": "MB/s (decoded bytes)",
-               "ms_per_step": round(ddt / a.decode_steps * 1e3, 3), "steps": a.decode_steps,
+        dec = {"value": round(dres["in_bytes"] * a.decode_steps / dres["dt"] / 1e6, 2), "unit": "MB/s (decoded bytes)",
+               "ms_per_step": round(dres["dt"] / a.decode_steps * 1e3, 3), "steps": a.decode_steps,
                "roundtrip_bit_exact": bool(ok)}
         d_dec.free()
-    in_bytes = float(total) * world
-    # parity spot check: this rank's first block vs the reference manifest
-    parity = None
-    if bs == 1 << 22:
-        sys.path.insert(0, os.path.join(REPO, "tests"))
-        try:
-            from oracle_ffi import manifest
-            man = manifest("random_1g_4m")["blocks"]
-            checks = [(i, b) for i, b in enumerate(mine) if b < len(man)][:4]
-            okc = 0
-            for i, b in checks:
-                rec = d_out.download(int(ro[i + 1] - ro[i]), int(ro[i]))
-                okc += hashlib.sha256(rec.tobytes()).hexdigest() == man[b]["sha256"]
-            parity = f"{okc}/{len(checks)} records byte-identical to the reference manifest"
-        except Exception as e:
-            parity = f"unchecked ({e})"
+
+    pcie = pcie_leg(r, enc, a.pcie_steps, 1) if a.pcie_steps > 0 else None
+    cal = calgary_leg(ctx, a.calgary_steps) if (a.calgary_steps > 0 and r.rank == 0) else None
 
     if r.rank == 0:
-        steps = a.steps
-        value = in_bytes * steps / dt / 1e6
-        # dominant kernel over the timed region
-        dom = max(stats.items(), key=lambda kv: kv[1][1]) if stats else None
-        roof = None
-        if dom:
-            name, (launches, ms) = dom
-            lps = launches / ksteps
-            avg_s = ms / launches / 1e3
-            per_launch = ALGO_BYTES_PER_INPUT_BYTE * total / lps  # batch bytes per launch
-            ach = per_launch / avg_s / 1e9
-            traffic = None
-            try:  # HBM bytes per launch from the committed PMC summary of this workload
-                pm = json.load(open(PMC_TRAFFIC))
-                if pm.get("workload_bytes") == total and name in pm.get("kernels", {}):
-                    traffic = pm["kernels"][name]["hbm_bytes_per_launch"]
-            except (OSError, ValueError, KeyError):
-                pass
-            stage = STAGE_BYTES_PER_INPUT_BYTE.get(name)
-            roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "measured": "HIP events on the kernel's stream, 1-stream kernel pass of the same workload",
-                    "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": name,
-                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches_per_step": lps,
-                    "algorithmic_bytes_per_launch": per_launch,
-                    "stage_model_bytes_per_launch": stage * total if stage else None,
-                    "stage_model_frac": round(stage * total / avg_s / 1e9 / HBM_PEAK_GBS, 4) if stage else None}
+        steps, dt = a.steps, res["dt"]
+        value = res["in_bytes"] * steps / dt / 1e6
+        wl = ("BASELINE config 4: 1 GiB uniform-random bytes per GPU, 4 MiB blocks, round-robin block deal"
+              if a.scaling == "weak" else
+              f"BASELINE config 4: {a.total_bytes >> 20} MiB uniform-random bytes in total, 4 MiB blocks dealt "
+              f"round-robin over {world} GPU(s)")
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": steps,
             "warmup": a.warmup, "ms_per_step": round(dt / steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: splitmix64(seed 0) bytes (SURVEY App. D), generated in HBM",
-            "config": {"workload": "BASELINE config 4: 1 GiB uniform-random bytes per GPU, 4 MiB blocks, "
-                                   "round-robin block deal", "block_size": bs, "blocks_per_gpu": nblk,
-                       "bytes_per_gpu": total, "parallelism": f"{world} independent GPU(s), no collective",
+            "config": {"workload": wl, "block_size": bs, "blocks_per_gpu": len(mine),
+                       "bytes_per_gpu": enc.in_bytes, "parallelism": f"{world} independent GPU(s), no collective",
                        "streams_per_gpu": int(os.environ.get("BMH_STREAMS", "2"))},
-            "ratio": round(out_bytes / in_bytes, 7),
-            "roofline": roof,
+            "ratio": round(res["out_bytes"] / res["in_bytes"], 7),
+            "device_only_graded_frac": round(value / 1e3 / (world * HBM_PEAK_GBS), 6),
+            "pcie_inclusive": pcie,
+            "calgary": cal,
+            "roofline": roofline(stats, ksteps, enc.in_bytes),
             "kernels_ms_per_step": {k: round(v[1] / ksteps, 3) for k, v in sorted(stats.items(), key=lambda kv: -kv[1][1])},
             "host_wall_ms_per_step": {k: round(v[1] / ksteps, 3) for k, v in walls.items()},
             "parity": parity,
             "decode": dec,
         }
         if world == 1 and not a.no_cpu_baseline:
-            ns = a.cpu_sample or min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 8)))
-            line["cpu_baseline"] = cpu_baseline(bs, ns)
+            line["cpu_baseline"] = cpu_baseline(bs, a.cpu_procs or None)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -62,6 +62,8 @@ _SIGS = {
     "bmh_ctx_stream": (P, [P]),
     "bmh_dev_alloc": (C.c_int, [P, U64, C.POINTER(P)]),
     "bmh_dev_free": (C.c_int, [P, P]),
+    "bmh_host_alloc": (C.c_int, [P, U64, C.POINTER(P)]),
+    "bmh_host_free": (C.c_int, [P, P]),
     "bmh_memcpy_h2d": (C.c_int, [P, P, P, U64]),
     "bmh_memcpy_d2h": (C.c_int, [P, P, P, U64]),
     "bmh_bwt_dev": (C.c_int, [P, P, PU64, U32, P, PU64]),
@@ -156,6 +158,30 @@ class DevBuf:
             pass
 
 
+class HostBuf:
+    """Page-locked host memory (bmh_host_alloc) viewed as a numpy uint8 array (`.a`)."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = C.c_void_p()
+        _check(lib().bmh_host_alloc(ctx.h, max(1, self.nbytes), C.byref(p)), "host_alloc")
+        self.ptr = p
+        self.a = np.ctypeslib.as_array((C.c_uint8 * max(1, self.nbytes)).from_address(p.value))[: self.nbytes]
+
+    def free(self) -> None:
+        if self.ptr:
+            self.a = None
+            lib().bmh_host_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "ptr", None) and self.ctx.h:
+                self.free()
+        except Exception:
+            pass
+
+
 class Context:
     """One GPU (bmh_ctx). Not thread-safe; use one per device/thread."""
 
@@ -184,6 +210,17 @@ class Context:
 
     def alloc(self, nbytes: int) -> DevBuf:
         return DevBuf(self, nbytes)
+
+    def alloc_host(self, nbytes: int) -> HostBuf:
+        return HostBuf(self, nbytes)
+
+    def compress_into(self, src: np.ndarray, block_size: int, out: np.ndarray) -> int:
+        """bmh_compress_host from `src` into `out` (numpy uint8 views, e.g. HostBuf.a for the
+        DMA-only path); returns the output length."""
+        n = C.c_uint64()
+        _check(lib().bmh_compress_host(self.h, _ptr(src), src.size, block_size, _ptr(out), out.size, C.byref(n)),
+               "compress_host")
+        return n.value
 
     # ---- measurement
     def set_timing(self, on: bool) -> None:

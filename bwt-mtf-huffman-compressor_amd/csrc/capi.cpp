@@ -353,6 +353,22 @@ static unsigned copy_threads()
     return std::min(16u, hw);
 }
 
+// Page-locked (hipHostMalloc'd or hipHostRegister'ed) host range: the DMA engines read and
+// write it directly, so the streaming encoder skips its staging copies.
+static bool is_pinned(const void *p, uint64_t bytes)
+{
+    if (!p || bytes == 0) return false;
+    for (const uint8_t *q : {(const uint8_t *)p, (const uint8_t *)p + bytes - 1}) {
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (a.type != hipMemoryTypeHost) return false;
+    }
+    return true;
+}
+
 static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes)
 {
     if (!c->s_h2d) BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
@@ -387,11 +403,20 @@ struct RecRef {
 };
 
 // Receives the records of consecutive entries [i0, i0 + cnt) of the block list: record j at
-// src + ro[j] .. src + ro[j + 1] (pinned staging; valid only during the call).
+// src + ro[j] .. src + ro[j + 1] (pinned staging, valid only during the call; or, with a
+// pinned destination, their final place).
 using RecordSink = std::function<void(size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro)>;
 
+// Pinned fast path (the caller's buffers are page-locked): `in_pinned` issues the H2D copies
+// straight from the caller's input; a PinnedOut lets the D2H copies land the records at their
+// final place, back to back from `at` (capacity `cap`), with no host copy at all.
+struct PinnedOut {
+    uint8_t *base = nullptr;
+    uint64_t cap = 0, at = 0;
+};
+
 static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t bs, const std::vector<uint64_t> &blist,
-                               const RecordSink &sink)
+                               const RecordSink &sink, bool in_pinned = false, PinnedOut *pout = nullptr)
 {
     struct B {
         std::vector<uint64_t> blocks, offs;
@@ -423,7 +448,8 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
         max_in = std::max(max_in, bt.offs.back());
         max_cap = std::max(max_cap, bt.cap);
     }
-    ensure_staging(c, max_in, max_cap);
+    ensure_staging(c, in_pinned ? 1 : max_in, pout ? 1 : max_cap);
+    std::vector<uint8_t *> dst(K, nullptr);  // pinned destination of each batch's records
     uint8_t *d_in[2] = {(uint8_t *)c->get(WS_IN, max_in), (uint8_t *)c->get(WS_IN2, max_in)};
     uint8_t *d_out[2] = {(uint8_t *)c->get(WS_OUT, max_cap), (uint8_t *)c->get(WS_OUT2, max_cap)};
     hipEvent_t ev_h2d[2], ev_d2h[2];
@@ -485,10 +511,15 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
             for (size_t i = 0; i < bt.blocks.size();) {
                 size_t j = i + 1;
                 while (j < bt.blocks.size() && bt.blocks[j] == bt.blocks[j - 1] + 1) ++j;
-                par_memcpy(c->stage_in[s] + bt.offs[i], in + bt.blocks[i] * bs, bt.offs[j] - bt.offs[i], nt);
+                if (in_pinned)
+                    BMH_HIP(hipMemcpyAsync(d_in[s] + bt.offs[i], in + bt.blocks[i] * bs, bt.offs[j] - bt.offs[i],
+                                           hipMemcpyHostToDevice, c->s_h2d));
+                else
+                    par_memcpy(c->stage_in[s] + bt.offs[i], in + bt.blocks[i] * bs, bt.offs[j] - bt.offs[i], nt);
                 i = j;
             }
-            BMH_HIP(hipMemcpyAsync(d_in[s], c->stage_in[s], bt.offs.back(), hipMemcpyHostToDevice, c->s_h2d));
+            if (!in_pinned)
+                BMH_HIP(hipMemcpyAsync(d_in[s], c->stage_in[s], bt.offs.back(), hipMemcpyHostToDevice, c->s_h2d));
             BMH_HIP(hipEventRecord(ev_h2d[s], c->s_h2d));
             bump(loaded);
         }
@@ -498,7 +529,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
             const int s = (int)(k & 1);
             if (!wait_for([&] { return d2h_issued > k; })) return;
             BMH_HIP(hipEventSynchronize(ev_d2h[s]));
-            sink(first[k], batches[k].blocks.size(), c->stage_out[s], ro[k].data());
+            sink(first[k], batches[k].blocks.size(), pout ? dst[k] : c->stage_out[s], ro[k].data());
             bump(written);
         }
     }));
@@ -514,8 +545,14 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
             encode_blocks(c, d_in[s], b, d_out[s], bt.cap, ro[k].data());
             bump(encoded);
             if (!wait_for([&] { return written + 2 > k; })) return;  // the writer is done with stage_out[s]
-            BMH_HIP(hipMemcpyAsync(c->stage_out[s], d_out[s], ro[k][bt.blocks.size()], hipMemcpyDeviceToHost,
-                                   c->s_d2h));
+            const uint64_t bytes = ro[k][bt.blocks.size()];
+            uint8_t *to = c->stage_out[s];
+            if (pout) {
+                if (pout->at + bytes > pout->cap) fail(BMH_ERANGE, "compress: output capacity too small");
+                to = dst[k] = pout->base + pout->at;
+                pout->at += bytes;
+            }
+            BMH_HIP(hipMemcpyAsync(to, d_out[s], bytes, hipMemcpyDeviceToHost, c->s_d2h));
             BMH_HIP(hipEventRecord(ev_d2h[s], c->s_d2h));
             bump(d2h_issued);
         }
@@ -697,6 +734,28 @@ bmh_status bmh_dev_free(bmh_ctx *c, void *d_ptr)
     API_END
 }
 
+bmh_status bmh_host_alloc(bmh_ctx *c, uint64_t bytes, void **h_ptr)
+{
+    API_BEGIN
+    use_device(c);
+    if (!h_ptr) fail(BMH_EINVAL, "null argument");
+    *h_ptr = nullptr;
+    if (hipHostMalloc(h_ptr, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        *h_ptr = nullptr;
+        fail(BMH_ENOMEM, "pinned host allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    API_END
+}
+
+bmh_status bmh_host_free(bmh_ctx *c, void *h_ptr)
+{
+    API_BEGIN
+    use_device(c);
+    if (h_ptr) BMH_HIP(hipHostFree(h_ptr));
+    API_END
+}
+
 bmh_status bmh_memcpy_h2d(bmh_ctx *c, void *d_dst, const void *h_src, uint64_t bytes)
 {
     API_BEGIN
@@ -824,6 +883,8 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
     // one context: records go straight from the staging slots to their place in `out`
     const bool direct = nctx == 1;
     const uint64_t table = nblocks == 1 ? 0 : 32 + 8 * nblocks;
+    use_device(ctxs[0]);
+    const bool in_pinned = is_pinned(in, n), out_pinned = direct && is_pinned(out, out_cap);
     uint64_t at = table;
     if (direct && table > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
     std::vector<bmh_status> st(nctx, BMH_OK);
@@ -833,16 +894,19 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
             std::vector<uint64_t> bl;
             for (uint64_t b = g; b < nblocks; b += nctx) bl.push_back(b);
             if (direct) {
-                encode_host_blocks(ctxs[g], in, n, bs, bl,
-                                   [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
-                                       const uint64_t bytes = ro[cnt];
-                                       if (at + bytes > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
-                                       par_memcpy(out + at, src, bytes, copy_threads());
-                                       for (size_t i = 0; i < cnt; ++i) {
-                                           if (table) put_u64(out + 32 + 8 * (i0 + i), ro[i + 1] - ro[i]);
-                                       }
-                                       at += bytes;
-                                   });
+                PinnedOut po{out, out_cap, table};
+                encode_host_blocks(
+                    ctxs[g], in, n, bs, bl,
+                    [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
+                        const uint64_t bytes = ro[cnt];
+                        if (at + bytes > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
+                        if (src != out + at) par_memcpy(out + at, src, bytes, copy_threads());
+                        for (size_t i = 0; i < cnt; ++i) {
+                            if (table) put_u64(out + 32 + 8 * (i0 + i), ro[i + 1] - ro[i]);
+                        }
+                        at += bytes;
+                    },
+                    in_pinned, out_pinned ? &po : nullptr);
             } else {
                 encode_host_blocks(ctxs[g], in, n, bs, bl,
                                    [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
@@ -852,7 +916,8 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
                                        for (size_t i = 0; i < cnt; ++i)
                                            recs[bl[i0 + i]] = RecRef{buf.get() + ro[i], ro[i + 1] - ro[i]};
                                        store[g].push_back(std::move(buf));
-                                   });
+                                   },
+                                   in_pinned);
             }
         } catch (const Error &e) {
             st[g] = e.status;

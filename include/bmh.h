@@ -61,6 +61,10 @@ void *bmh_ctx_stream(bmh_ctx *ctx);
 /* Device memory helpers (so FFI callers need no HIP headers). */
 bmh_status bmh_dev_alloc(bmh_ctx *ctx, uint64_t bytes, void **d_ptr);
 bmh_status bmh_dev_free(bmh_ctx *ctx, void *d_ptr);
+/* Page-locked host memory (hipHostMalloc). bmh_compress_host detects page-locked input and
+ * output buffers and then moves the data by DMA only: no staging copies on the host. */
+bmh_status bmh_host_alloc(bmh_ctx *ctx, uint64_t bytes, void **h_ptr);
+bmh_status bmh_host_free(bmh_ctx *ctx, void *h_ptr);
 bmh_status bmh_memcpy_h2d(bmh_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);
 bmh_status bmh_memcpy_d2h(bmh_ctx *ctx, void *h_dst, const void *d_src, uint64_t bytes);
 
@@ -108,7 +112,8 @@ uint64_t bmh_record_bound(uint64_t n);
 /* ---- host-buffer convenience (H2D + encode + D2H) ---------------------------------- */
 /* Encodes `in` (n bytes) cut into block_size blocks (block_size 0 or >= n: one block).
  * One block => exactly the reference record; several => the BMH container (bmh_container_*).
- * Returns the output size in *out_len. */
+ * Returns the output size in *out_len. Batches stream through H2D / encode / D2H on separate
+ * streams; with page-locked `in` / `out` (bmh_host_alloc) the copies are DMA-only. */
 bmh_status bmh_compress_host(bmh_ctx *ctx, const uint8_t *in, uint64_t n, uint64_t block_size,
                              uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 /* Same, spreading blocks round-robin (block b -> ctxs[b % nctx]) over several contexts

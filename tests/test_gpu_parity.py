@@ -472,6 +472,37 @@ def test_device_errors_are_status_codes(ctx):
     assert ctx.decompress_bytes(ctx.encode_blocks([a.tobytes()])[0]) == a.tobytes()
 
 
+def test_compress_host_pinned_buffers(ctx, monkeypatch):
+    """bmh_compress_host with page-locked input and output (bmh_host_alloc: DMA-only path,
+    records D2H'd straight to their place) writes the same bytes as with pageable buffers;
+    several stream batches, a single block, and a too-small page-locked output (ERANGE)."""
+    monkeypatch.setenv("BMH_STREAM_BATCH", str(3 << 20))
+    data = np.frombuffer(synth.zipf_text(10_000_019).tobytes(), np.uint8)
+    hin = ctx.alloc_host(data.size)
+    hin.a[:] = data
+    try:
+        for bs in (1 << 20, 1 << 24):
+            ref = ctx.compress_bytes(data, block_size=bs)
+            cap = int(bmh.lib().bmh_compress_bound(data.size, bs))
+            hout = ctx.alloc_host(cap)
+            n = ctx.compress_into(hin.a, bs, hout.a)
+            assert hout.a[:n].tobytes() == ref, bs
+            n2 = ctx.compress_into(data, bs, hout.a)  # pageable in, pinned out
+            assert hout.a[:n2].tobytes() == ref, bs
+            out = np.empty(cap, np.uint8)
+            n3 = ctx.compress_into(hin.a, bs, out)  # pinned in, pageable out
+            assert out[:n3].tobytes() == ref, bs
+            hout.free()
+        small = ctx.alloc_host(1000)
+        with pytest.raises(bmh.BmhError) as e:
+            ctx.compress_into(hin.a, 1 << 20, small.a)
+        assert e.value.status == 4  # BMH_ERANGE
+        small.free()
+        assert ctx.decompress_bytes(ctx.compress_bytes(data[:5000], 0)) == data[:5000].tobytes()
+    finally:
+        hin.free()
+
+
 def test_compress_host_multi_matches_single_context(ctx):
     """bmh_compress_host_multi (one context + host thread each, blocks dealt round-robin)
     assembles the same container as one context; here several contexts share the test GPU.
