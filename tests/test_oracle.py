@@ -10,7 +10,9 @@ import numpy as np
 import pytest
 
 from bmh import synth
-from oracle_ffi import golden_calgary, golden_small, manifest
+import os
+
+from oracle_ffi import GOLDEN, golden_calgary, golden_small, manifest
 
 # (primary, tree bytes, payload bytes, total) per Calgary file
 APPENDIX_C = {
@@ -107,3 +109,20 @@ def test_synth_hashes():
     z = synth.zipf_text(16 << 20)
     assert hashlib.sha256(z.tobytes()).hexdigest() == \
         "b8b5a2980d7a3c0ec97b8eafa08eaf2423aa1696be1fb47b191566c737d2b889"
+
+
+def test_full_pipeline_fixture_sizes_and_decode(oracle):
+    """The reference's FULL_PIPELINE records (tests/golden/full_pipeline, make_full_pipeline.py):
+    same sizes and headers as its standalone COMPRESS records, tree bytes may differ (heap
+    history across files); each decodes to its input with the oracle and the host decoder."""
+    import bmh
+    fp = os.path.join(GOLDEN, "full_pipeline")
+    differ = 0
+    for name, data, rec in golden_calgary():
+        with open(os.path.join(fp, name + ".bzap"), "rb") as f:
+            full = f.read()
+        assert len(full) == len(rec) and full[:24] == rec[:24], name
+        differ += full != rec
+        assert oracle.decode(full) == data, name
+        assert bmh.decompress_bytes(full) == data, name
+    assert differ == 13
