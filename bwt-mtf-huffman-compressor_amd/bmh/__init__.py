@@ -88,6 +88,7 @@ _SIGS = {
     "bmh_ctx_reset_stats": (C.c_int, [P]),
     "bmh_ctx_kernel_stats": (C.c_int, [P, P, PU64, C.POINTER(C.c_double), C.c_int]),
     "bmh_synth_splitmix64_dev": (C.c_int, [P, P, U64, U64, U64]),
+    "bmh_check_violations": (C.c_int64, [P, U32]),
 }
 
 

@@ -18,6 +18,11 @@
 
 namespace bmh {
 
+// Checked builds (-DBMH_CHECK): kinds of device-side precondition violations (device_util.h)
+// and the registry of per-translation-unit readers (capi.cpp, bmh_check_violations).
+enum : uint32_t { kCheckExec = 0, kCheckKinds = 4 };
+void check_register(uint32_t (*reader)(uint32_t kind));
+
 struct Error : std::runtime_error {
     bmh_status status;
     Error(bmh_status s, const std::string &m) : std::runtime_error(m), status(s) {}

@@ -602,6 +602,14 @@ static void assemble(uint64_t n, uint64_t bs, uint64_t nblocks, const std::vecto
     *out_len = total;
 }
 
+// Checked builds: every kernel translation unit registers the reader of its violation table.
+static std::vector<uint32_t (*)(uint32_t)> &check_readers()
+{
+    static std::vector<uint32_t (*)(uint32_t)> v;
+    return v;
+}
+void check_register(uint32_t (*reader)(uint32_t kind)) { check_readers().push_back(reader); }
+
 }  // namespace bmh
 
 using namespace bmh;
@@ -636,6 +644,26 @@ static void use_device(bmh_ctx *c)
 extern "C" {
 
 const char *bmh_version(void) { return "bmh 0.1.0 (gfx950)"; }
+
+int64_t bmh_check_violations(bmh_ctx *c, uint32_t kind)
+{
+#ifdef BMH_CHECK
+    if (!c || kind >= kCheckKinds || hipSetDevice(c->device) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        return -2;
+    if (check_readers().empty()) return -2;
+    int64_t tot = 0;
+    for (auto *r : check_readers()) {
+        const uint32_t v = r(kind);
+        if (v == 0xffffffffu) return -2;
+        tot += v;
+    }
+    return tot;
+#else
+    (void)c;
+    (void)kind;
+    return -1;
+#endif
+}
 
 const char *bmh_status_str(int s)
 {
@@ -873,6 +901,13 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
 {
     API_BEGIN
     if (!ctxs || nctx == 0 || !in || !out || !out_len) fail(BMH_EINVAL, "null argument");
+    // each context is driven by its own host thread: a context listed twice would be used by
+    // two threads at once (several contexts may share one device: they time-share it)
+    for (uint32_t g = 0; g < nctx; ++g) {
+        if (!ctxs[g]) fail(BMH_EINVAL, "null context in the list");
+        for (uint32_t h = 0; h < g; ++h)
+            if (ctxs[h] == ctxs[g]) fail(BMH_EINVAL, "context listed twice");
+    }
     if (n == 0) fail(BMH_EINVAL, "empty input (the reference segfaults on empty input)");
     const uint64_t bs = (block_size == 0 || block_size >= n) ? n : block_size;
     if (bs >= 0xffffffffull) fail(BMH_ERANGE, "block size must be < 4 GiB - 1");

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "bmh_internal.h"
+
 namespace bmh {
 
 constexpr int kWave = 64;
@@ -15,6 +17,30 @@ __device__ __forceinline__ uint32_t writelane(uint32_t val, uint32_t lane, uint3
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63u; }
+
+// Checked builds (-DBMH_CHECK, `make check`): device-side preconditions are counted, never
+// trapped, in a per-translation-unit table the host reads through bmh_check_violations().
+//   kCheckExec: a full-wave primitive (DPP scans, the one-barrier workgroup scan) ran with
+//   a partial EXEC mask — inactive lanes feed stale values into the DPP row shifts and
+//   broadcasts, so the sums (and every slot derived from them) are wrong.
+#ifdef BMH_CHECK
+namespace {
+__device__ uint32_t g_check_bad[kCheckKinds];
+uint32_t check_read_tu(uint32_t kind)
+{
+    uint32_t v[kCheckKinds] = {};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(g_check_bad), sizeof(v)) != hipSuccess) return 0xffffffffu;
+    return v[kind];
+}
+const bool check_registered = (check_register(&check_read_tu), true);
+}  // namespace
+__device__ __forceinline__ void check_full_exec()
+{
+    if (__builtin_amdgcn_read_exec() != ~0ull) atomicAdd(&g_check_bad[kCheckExec], 1u);
+}
+#else
+__device__ __forceinline__ void check_full_exec() {}
+#endif
 
 // Ordering point for LDS data that only the calling wave reads and writes: a wave's LDS
 // operations execute in order, so no barrier is needed, only that the compiler keeps the
@@ -102,6 +128,7 @@ __device__ __forceinline__ uint32_t wave_incl_min_rev(uint32_t x)  // suffix min
 // lane of the wave must be active.
 __device__ __forceinline__ uint32_t wave_incl_sum_dpp(uint32_t x)
 {
+    check_full_exec();
     // update_dpp(old, src, ctrl, row_mask, bank_mask, bound_ctrl): lanes whose source is out of
     // the row, and rows outside row_mask, get `old` = 0
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -126,6 +153,7 @@ template <int NT>
 __device__ __forceinline__ uint32_t block_excl_sum1(uint32_t v, uint32_t *s_tmp, uint32_t *total = nullptr)
 {
     constexpr int NW = NT / 64;
+    check_full_exec();
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t inc = wave_incl_sum_dpp(v);
     if (lane_id() == 63) s_tmp[w] = inc;

@@ -156,6 +156,11 @@ bmh_status bmh_ctx_reset_stats(bmh_ctx *ctx);
 /* Kernel stats: returns how many distinct kernels were recorded; fills up to cap entries. */
 int bmh_ctx_kernel_stats(bmh_ctx *ctx, char (*names)[64], uint64_t *launches, double *total_ms, int cap);
 
+/* Checked builds (`make check` -> lib_check/libbmh.so, -DBMH_CHECK): number of device-side
+ * precondition violations of `kind` so far (0: a full-wave primitive ran with a partial EXEC
+ * mask). -1 in a regular build, -2 on error. Not part of the reference interface (test aid). */
+int64_t bmh_check_violations(bmh_ctx *ctx, uint32_t kind);
+
 /* Synthetic input: bytes [offset, offset+nbytes) of the little-endian
  * splitmix64(seed) stream, generated on the device. */
 bmh_status bmh_synth_splitmix64_dev(bmh_ctx *ctx, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);

@@ -165,3 +165,40 @@ def test_huffman_build_long_codes_matches_oracle(oracle, nsym):
     assert (code[oln > 0] == ocode[oln > 0]).all()
     assert t.tree_bytes == otree
     assert bmh.payload_bytes(t, freq) == max(1, (int((freq * ln.astype(np.uint64)).sum()) + 7) // 8)
+
+
+ASAN_BIN = os.path.join(REPO, "bwt-mtf-huffman-compressor_amd", "bin", "host_asan")
+
+
+def test_host_code_under_asan_ubsan():
+    """SURVEY §5 (race detection / sanitizers): the host sources of libbmh (record decode,
+    container framing, Huffman code books, status paths) built with ASan + UBSan
+    (`make asan`; device code unsanitised) and driven by tests/asan/host_asan.cpp over golden
+    records, every header truncation, edge-valued header fields, random byte flips and damaged
+    container tables. Any overrun or UB aborts the driver."""
+    pkg = os.path.join(REPO, "bwt-mtf-huffman-compressor_amd")
+    b = subprocess.run(["make", "-C", pkg, "asan"], capture_output=True, text=True, timeout=900)
+    assert b.returncode == 0, b.stdout[-2000:] + b.stderr[-2000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    names = ["bib", "paper1", "paper2", "progc", "progl", "progp", "trans", "obj1", "geo"]
+    r = subprocess.run([ASAN_BIN, GOLDEN] + names, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "0 failure(s)" in r.stdout
+
+
+def test_compress_host_multi_rejects_bad_context_lists():
+    """bmh_compress_host_multi drives each context from its own host thread: a context listed
+    twice, or a null entry, is refused (BMH_EINVAL) before any device is touched."""
+    import ctypes as C
+    L = bmh.lib()
+    data = np.frombuffer(b"banana" * 100, np.uint8)
+    out = np.zeros(4096, np.uint8)
+    olen = np.zeros(1, np.uint64)
+    fake = C.c_void_p(0x1000)
+    for lst in ([fake, fake], [fake, C.c_void_p(0)]):
+        arr = (C.c_void_p * len(lst))(*lst)
+        st = L.bmh_compress_host_multi(arr, len(lst), data.ctypes.data, data.size, 64, out.ctypes.data, out.size,
+                                       olen.ctypes.data_as(bmh.PU64))
+        assert st == bmh.BMH_EINVAL
+        assert "context" in L.bmh_last_error().decode()
