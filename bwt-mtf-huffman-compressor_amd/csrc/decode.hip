@@ -601,10 +601,10 @@ __device__ __forceinline__ uint32_t e_l(uint64_t e) { return (uint32_t)(e >> 32)
 template <typename ET>
 __global__ __launch_bounds__(256) void k_lf_rank(const uint8_t *__restrict__ L, const DBlock *__restrict__ blks,
                                                  const uint32_t *__restrict__ ch_block,
-                                                 const uint32_t *__restrict__ chist, ET *__restrict__ E)
+                                                 const uint32_t *__restrict__ chist, ET *__restrict__ E, uint32_t c0)
 {
     __shared__ uint32_t s_wcnt[4][256];
-    const uint32_t c = blockIdx.x, b = ch_block[c];
+    const uint32_t c = c0 + blockIdx.x, b = ch_block[c];
     const DBlock B = blks[b];
     const uint32_t r0 = (c - B.ch0) * kLfChunk, len = min(kLfChunk, B.n - r0);
     const uint8_t *Lb = L + B.out_off + r0;
@@ -668,13 +668,13 @@ constexpr uint32_t kSlot = 1024;
 
 template <typename ET>
 __global__ __launch_bounds__(256) void k_lf_walk1(const DBlock *__restrict__ blks, const uint32_t *__restrict__ sp_block,
-                                                  uint32_t nsp_total, const ET *__restrict__ E,
+                                                  uint32_t g0, uint32_t g1, const ET *__restrict__ E,
                                                   uint32_t *__restrict__ nxt, uint64_t *__restrict__ dist,
                                                   uint32_t *__restrict__ resume, uint8_t *__restrict__ tmp,
                                                   uint32_t *status)
 {
-    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
-    if (g >= nsp_total) return;
+    const uint32_t g = g0 + blockIdx.x * 256 + threadIdx.x;
+    if (g >= g1) return;
     const uint32_t b = sp_block[g];
     const DBlock B = blks[b];
     const uint32_t id = g - B.sp0;
@@ -686,14 +686,20 @@ __global__ __launch_bounds__(256) void k_lf_walk1(const DBlock *__restrict__ blk
     }
     const ET *Eb = E + B.out_off;
     uint8_t *slot = tmp + (size_t)g * kSlot;
+    // the segment's first kSlot characters go to the slot 16 bytes at a time (4-byte stores
+    // from every thread to its own slot cost a partial-line write each)
     uint32_t r = r0, len = 0, sid, acc = 0;
+    uint32_t q[4] = {0, 0, 0, 0};
     do {
         const ET e = Eb[r];
         if (len < kSlot) {
             acc |= e_l(e) << (8 * (len & 3u));
             if ((len & 3u) == 3u) {
-                *(uint32_t *)(slot + len - 3) = acc;
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (((len >> 2) & 3u) == j) q[j] = acc;
                 acc = 0;
+                if ((len & 15u) == 15u) *(uint4 *)(slot + len - 15) = make_uint4(q[0], q[1], q[2], q[3]);
             }
         } else if (len == kSlot) {
             resume[g] = r;
@@ -702,7 +708,12 @@ __global__ __launch_bounds__(256) void k_lf_walk1(const DBlock *__restrict__ blk
         ++len;
         sid = split_id(r, B);
     } while (sid == kNil && len <= B.n);
-    if (len < kSlot && (len & 3u)) *(uint32_t *)(slot + (len & ~3u)) = acc;
+    if (len < kSlot && (len & 15u)) {  // the partial last piece (its unused bytes are never read)
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (((len >> 2) & 3u) == j) q[j] = acc;
+        *(uint4 *)(slot + (len & ~15u)) = make_uint4(q[0], q[1], q[2], q[3]);
+    }
     if (len > B.n || r >= B.n) {
         atomicOr(status, 2u);
         sid = kNil;
@@ -809,6 +820,8 @@ __global__ __launch_bounds__(256) void k_lf_place(const DBlock *__restrict__ blk
     }
     const uint8_t *slot = tmp + (size_t)g * kSlot;
     const uint64_t inslot = len < kSlot ? len : kSlot;
+    // (byte stores: aligned word stores with the slot read by aligned words measured slower,
+    // 6.7 against 4.8 ms per GiB)
     for (uint64_t t = 0; t < inslot; ++t) ob[pos - 1 - t] = slot[t];
     if (len > kSlot) {
         const ET *Eb = E + B.out_off;
@@ -862,13 +875,17 @@ void lf_inverse(Ctx *c, const std::vector<DBlock> &hb, uint32_t nb, uint64_t tot
     ET *d_E = (ET *)c->get(WS_KEY8, total * sizeof(ET) + 64);
     BMH_LAUNCH(c, "dec_lf_hist", k_lf_hist, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist);
     BMH_LAUNCH(c, "dec_lf_scan", k_lf_scan, nb, 256, 0, d_blk, d_chist);
-    BMH_LAUNCH(c, "dec_lf_rank", k_lf_rank<ET>, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist, d_E);
     uint8_t *d_sp = (uint8_t *)c->get(WS_RKA, (size_t)nsp * 36 + 64);
     uint32_t *d_nxt = (uint32_t *)d_sp, *d_nxt2 = d_nxt + nsp, *d_resume = d_nxt2 + nsp;
     uint64_t *d_dist = (uint64_t *)(((uintptr_t)(d_resume + nsp) + 7) & ~(uintptr_t)7), *d_dist2 = d_dist + nsp;
     uint64_t *d_len = (uint64_t *)c->get(WS_RKB, (size_t)nsp * 8 + 64);
     uint8_t *d_tmp = (uint8_t *)c->get(WS_KEY, (size_t)nsp * kSlot + 64);
-    BMH_LAUNCH(c, "dec_lf_walk", k_lf_walk1<ET>, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, nsp, d_E, d_nxt, d_dist,
+    // (Ranking and walking groups of blocks whose E fits the 256 MiB Infinity Cache, one group
+    // after the other, measured slower at every group size, 64-224 MiB: 34-65 ms against 21 ms
+    // per GiB. The walk is bound by its random-request rate through the L2s, not by where the
+    // line is served from, and a group has too few walks in flight.)
+    BMH_LAUNCH(c, "dec_lf_rank", k_lf_rank<ET>, nch, 256, 0, d_L, d_blk, d_ch_block, d_chist, d_E, 0u);
+    BMH_LAUNCH(c, "dec_lf_walk", k_lf_walk1<ET>, cdiv(nsp, 256), 256, 0, d_blk, d_sp_block, 0u, nsp, d_E, d_nxt, d_dist,
                d_resume, d_tmp, d_status);
     BMH_HIP(hipMemcpyAsync(d_len, d_dist, (size_t)nsp * 8, hipMemcpyDeviceToDevice, c->stream));
     // pointer jumping until the primary's chain is ranked; splitters on other LF cycles
