@@ -955,33 +955,48 @@ struct DTile {
     uint32_t seg, start, len, pad;
 };
 
+// Big-list segments flagged kRunMode (Seg4.w bit 30) were left holding >= 3/4 of their parent by
+// the previous MSD pass (run-dominated data: a long run of one byte, e.g. the zero runs of a fax
+// image). Their pass digit is the position of the first bit where a rotation's window differs
+// from the segment's smallest window (order-preserving: sharing more bits with the minimum
+// means smaller), so a pass advances up to 64 bits instead of 8.
+constexpr uint32_t kRunMode = 1u << 30;
+__device__ __forceinline__ uint32_t seg_blk(uint32_t w) { return w & 0xffffu; }
+
 // Bits every rotation of an MSD segment shares below its depth (OR of window XORs against
-// the segment's first rotation); the digit of the pass is taken right after them. Each
+// the segment's first rotation), and its smallest window; the digit of the pass is taken right
+// after the shared bits (or, kRunMode, from the first difference to the smallest window). Each
 // rotation's 64-bit window is kept in kbuf (by slot) so the histogram and scatter passes read it
 // coalesced instead of gathering it from the text again.
 __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                             unsigned long long *__restrict__ segor, uint64_t *__restrict__ kbuf)
+                                             unsigned long long *__restrict__ segor, unsigned long long *__restrict__ segmin,
+                                             uint64_t *__restrict__ kbuf)
 {
     __shared__ uint32_t s_or[2];
+    __shared__ unsigned long long s_min;
     const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
-    const uint32_t boff = a.boffs[s.w], n = a.boffs[s.w + 1] - boff;
+    const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     if (threadIdx.x < 2) s_or[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_min = ~0ull;
     __syncthreads();
     const uint64_t w0 = rot_window(blk, n, a.sa[s.x], s.z);
-    uint64_t acc = 0;
+    uint64_t acc = 0, mn = ~0ull;
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
         const uint64_t w = rot_window(blk, n, a.sa[t.start + e], s.z);
         kbuf[t.start + e] = w;
         acc |= w ^ w0;
+        mn = w < mn ? w : mn;
     }
     if (acc) {
         atomicOr(&s_or[0], (uint32_t)acc);
         atomicOr(&s_or[1], (uint32_t)(acc >> 32));
     }
+    if (s.w & kRunMode) atomicMin(&s_min, (unsigned long long)mn);
     __syncthreads();
     if (threadIdx.x == 0 && (s_or[0] | s_or[1])) atomicOr(&segor[t.seg], ((unsigned long long)s_or[1] << 32) | s_or[0]);
+    if (threadIdx.x == 0 && (s.w & kRunMode)) atomicMin(&segmin[t.seg], s_min);
 }
 
 // depth of the pass digit: the segment depth plus its shared bits (64: no digit in the window)
@@ -998,19 +1013,30 @@ __device__ __forceinline__ uint32_t msd_digit(const uint64_t *kbuf, uint32_t j, 
     return cp <= 56 ? (uint32_t)((kbuf[j] << cp) >> 56) : (uint32_t)(rot_window(blk, n, p, depth + cp) >> 56);
 }
 
+// kRunMode digit: 0 for the smallest window, else 64 - (bits shared with it), in 1..64
+__device__ __forceinline__ uint32_t run_digit(uint64_t w, uint64_t wmin)
+{
+    const uint64_t x = w ^ wmin;
+    return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u;
+}
+
 __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
                                                const unsigned long long *__restrict__ segor,
+                                               const unsigned long long *__restrict__ segmin,
                                                const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
 {
     __shared__ uint32_t h[256];
     const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
-    const uint32_t boff = a.boffs[s.w], n = a.boffs[s.w + 1] - boff;
+    const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     const uint32_t cp = seg_cp(segor, t.seg);
     h[threadIdx.x] = 0;
     __syncthreads();
-    if (cp == 64) {
+    if (s.w & kRunMode) {
+        const uint64_t wmin = segmin[t.seg];
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) atomicAdd(&h[run_digit(kbuf[t.start + e], wmin)], 1u);
+    } else if (cp == 64) {
         if (threadIdx.x == 0) h[0] = t.len;
     } else {
         for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
@@ -1022,7 +1048,8 @@ __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restric
     thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
-// grid = nsegs; 256 threads (digits). Offsets in place; sub-segment routing.
+// grid = nsegs; 256 threads (digits). Offsets in place; sub-segment routing. A child left
+// with >= 3/4 of its parent and still too big for a finish pass goes on in kRunMode.
 __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint2 *__restrict__ segtiles,
                                                const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
                                                uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove)
@@ -1042,9 +1069,12 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
     const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
     stot[(size_t)blockIdx.x * 256 + d] = tot;
-    const uint32_t b = s.w, n = a.boffs[b + 1] - a.boffs[b];
+    const uint32_t b = seg_blk(s.w), n = a.boffs[b + 1] - a.boffs[b];
     const uint32_t cp = seg_cp(segor, blockIdx.x);
-    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)s.z + (cp == 64 ? 64u : cp + 8u), 0xffffffffull);
+    // depth of this thread's child: kRunMode digit d shares 64 - d bits with the minimum and
+    // differs in the next one (d = 0: all 64 window bits equal the minimum's)
+    const uint32_t add = (s.w & kRunMode) ? (d == 0 ? 64u : 64u - d + 1u) : (cp == 64 ? 64u : cp + 8u);
+    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)s.z + add, 0xffffffffull);
     const bool final_depth = (uint64_t)nd >= 8ull * n;
     __shared__ DeferQueue<256> dq;
     dq_init(dq);
@@ -1060,7 +1090,8 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
         } else if (len <= kBigCap) {
             dq_push(a, dq, gs, len, nd, b, n);
         } else {
-            dq_push_list(a, dq, make_uint4(gs, len, nd, b), kListBig);
+            const bool stuck = (uint64_t)len * 4 >= (uint64_t)s.y * 3;
+            dq_push_list(a, dq, make_uint4(gs, len, nd, b | (stuck ? kRunMode : 0u)), kListBig);
         }
     };
     if (nz == 1) {
@@ -1075,6 +1106,7 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
 
 __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
                                                   const unsigned long long *__restrict__ segor,
+                                                  const unsigned long long *__restrict__ segmin,
                                                   const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
                                                   const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
                                                   uint32_t *__restrict__ sa2)
@@ -1082,16 +1114,18 @@ __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__rest
     __shared__ uint32_t cur[256];
     const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
-    const uint32_t b = s.w, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     if (nomove[t.seg]) return;  // one digit only: nothing moves
     const uint32_t cp = seg_cp(segor, t.seg);
+    const bool runm = (s.w & kRunMode) != 0;
+    const uint64_t wmin = runm ? segmin[t.seg] : 0ull;
     cur[threadIdx.x] = thist[(size_t)blockIdx.x * 256 + threadIdx.x];
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
         const uint32_t j = t.start + e;
         const uint32_t p = a.sa[j];
-        const uint32_t d = msd_digit(kbuf, j, cp, blk, n, p, s.z);
+        const uint32_t d = runm ? run_digit(kbuf[j], wmin) : msd_digit(kbuf, j, cp, blk, n, p, s.z);
         const uint32_t slot = atomicAdd(&cur[d], 1u);
         sa2[slot] = p;
         if (stot[(size_t)t.seg * 256 + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
@@ -1837,14 +1871,16 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 c->h2d(d_segtiles, hst.data(), nbig * 8);
                 uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
                 uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
-                unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 8 + 64);
+                unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 16 + 64);
+                unsigned long long *segmin = segor + nbig;
                 BMH_HIP(hipMemsetAsync(segor, 0, (size_t)nbig * 8, c->stream));
+                BMH_HIP(hipMemsetAsync(segmin, 0xff, (size_t)nbig * 8, c->stream));
                 // the global-pass records are no longer read: their buffer holds the windows
-                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor, rec);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, rec, thist);
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec, thist);
                 BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, segor, thist, stot, d_nomove);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, rec, d_nomove, thist,
-                           stot, sa2);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec, d_nomove,
+                           thist, stot, sa2);
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
             }
             read_counters();
