@@ -49,7 +49,7 @@ struct KStat {
 enum Slot : int {
     WS_SA, WS_SA2, WS_RKA, WS_RKB, WS_KEY, WS_KEY2, WS_SEG_CUR, WS_SEG_NXT, WS_TINY, WS_MED,
     WS_LARGE, WS_LARGE2, WS_GROUPS, WS_PREFIX, WS_SCAN_PART, WS_TILES, WS_BLOCKS, WS_OFFS,
-    WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_LISTS, WS_L, WS_MTF,
+    WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
     WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_COUNT_

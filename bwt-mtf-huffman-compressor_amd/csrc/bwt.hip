@@ -65,7 +65,10 @@ struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
     uint32_t lcnt[5];  // data phase: entries of each list (kListTiny .. kListGroups)
     uint32_t big, dmin_bits, flagged;
+    uint32_t coop_fill, coop_groups;  // groups too long for one wave (k_group_fill / k_groups)
 };
+constexpr uint32_t kCoopGroup = 8192;  // a group this long is walked by the whole grid
+constexpr uint32_t kCoopGrid = 1024;   // workgroups of the cooperative group kernels
 
 // Data-phase segment / group: {gstart (batch slot), len, bit depth, block (| kFinalFlag)}
 using Seg4 = uint4;
@@ -1161,31 +1164,54 @@ __global__ __launch_bounds__(256) void k_rank_fill(const uint32_t *__restrict__ 
 
 // Tied groups of the data phase: members get the group start as rank (flagged blocks);
 // identical-rotation (final) groups also get their L bytes / primary. Unresolved ones are
-// appended to the first doubling round's segment list. One wave per group.
+// appended to the first doubling round's segment list. One wave per group; groups longer than
+// kCoopGroup (long runs: a wave would walk 100 K+ rotations alone) are listed in `coop` for
+// k_group_fill_coop, which spreads each over the whole grid.
+__device__ __forceinline__ void group_fill_elem(const DataArgs &a, const Seg4 &s, uint32_t e, uint32_t *__restrict__ rkA,
+                                                uint32_t *__restrict__ rkB)
+{
+    const uint32_t b = s.w & ~kFinalFlag;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t p = a.sa[s.x + e];
+    if (a.bflag[b]) {
+        rkA[boff + p] = s.x - boff;
+        rkB[boff + p] = s.x - boff;
+    }
+    if (s.w & kFinalFlag) put_final(a, b, boff, n, a.data + boff, s.x + e, p, s.x - boff);
+}
+
 __global__ __launch_bounds__(256) void k_group_fill(DataArgs a, const Seg4 *__restrict__ groups, uint32_t ng,
                                                     uint32_t *__restrict__ rkA, uint32_t *__restrict__ rkB,
-                                                    uint2 *__restrict__ segs, Counters *cnt)
+                                                    uint2 *__restrict__ segs, uint32_t *__restrict__ coop, Counters *cnt)
 {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t l = threadIdx.x & 63u;
     for (uint32_t g = wave; g < ng; g += nwaves) {
         const Seg4 s = groups[g];
-        const uint32_t b = s.w & ~kFinalFlag;
-        const bool fin = (s.w & kFinalFlag) != 0;
-        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-        const uint8_t *blk = a.data + boff;
-        const bool ranks = a.bflag[b] != 0;
-        for (uint32_t e = l; e < s.y; e += 64) {
-            const uint32_t p = a.sa[s.x + e];
-            if (ranks) {
-                rkA[boff + p] = s.x - boff;
-                rkB[boff + p] = s.x - boff;
-            }
-            if (fin) put_final(a, b, boff, n, blk, s.x + e, p, s.x - boff);
+        if (s.y > kCoopGroup) {
+            if (l == 0) coop[atomicAdd(&cnt->coop_fill, 1u)] = g;
+            continue;
         }
-        if (!fin && l == 0) {
+        for (uint32_t e = l; e < s.y; e += 64) group_fill_elem(a, s, e, rkA, rkB);
+        if (!(s.w & kFinalFlag) && l == 0) {
             segs[wave_append(&cnt->next)] = make_uint2(s.x, s.y);
+            atomicMin(&cnt->dmin_bits, s.z);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_group_fill_coop(DataArgs a, const Seg4 *__restrict__ groups,
+                                                         const uint32_t *__restrict__ coop, uint32_t *__restrict__ rkA,
+                                                         uint32_t *__restrict__ rkB, uint2 *__restrict__ segs, Counters *cnt)
+{
+    const uint32_t nc = cnt->coop_fill;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    for (uint32_t i = 0; i < nc; ++i) {
+        const Seg4 s = groups[coop[i]];
+        for (uint32_t e = tid; e < s.y; e += nt) group_fill_elem(a, s, e, rkA, rkB);
+        if (!(s.w & kFinalFlag) && tid == 0) {
+            segs[atomicAdd(&cnt->next, 1u)] = make_uint2(s.x, s.y);
             atomicMin(&cnt->dmin_bits, s.z);
         }
     }
@@ -1237,7 +1263,8 @@ __device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32
 }
 
 __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 *__restrict__ tiny,
-                           uint2 *__restrict__ med, LSeg *__restrict__ large, Counters *cnt)
+                           uint2 *__restrict__ med, LSeg *__restrict__ large, Counters *cnt,
+                           const uint32_t *__restrict__ boffs, uint32_t nb)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nseg) return;
@@ -1248,9 +1275,11 @@ __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 
         med[wave_append(&cnt->med)] = s;
     } else {
         LSeg l;
+        // keys are block-local ranks (< n): the first MSD pass takes their highest nonzero byte
+        const uint32_t b = find_block(boffs, nb, s.x), n = boffs[b + 1] - boffs[b];
         l.gstart = s.x;
         l.len = s.y;
-        l.shift = 24;
+        l.shift = n > (1u << 24) ? 24u : n > (1u << 16) ? 16u : n > 256u ? 8u : 0u;
         l.gathered = 0;
         large[wave_append(&cnt->large)] = l;
     }
@@ -1578,18 +1607,37 @@ __global__ __launch_bounds__(256) void k_lcopy(const LTile *__restrict__ tiles, 
     }
 }
 
-// Groups produced by the large path (singletons, or key-exhausted equal-key groups).
-__global__ __launch_bounds__(256) void k_groups(RoundArgs a, const uint2 *__restrict__ groups, uint32_t ng)
+// Groups produced by the large path (singletons, or key-exhausted equal-key groups). One wave
+// per group; groups longer than kCoopGroup go to `coop` for k_groups_coop (the whole grid).
+__global__ __launch_bounds__(256) void k_groups(RoundArgs a, const uint2 *__restrict__ groups, uint32_t ng,
+                                                uint32_t *__restrict__ coop)
 {
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t l = threadIdx.x & 63u;
     for (uint32_t g = wave; g < ng; g += nwaves) {
         const uint2 s = groups[g];
+        if (s.y > kCoopGroup) {
+            if (l == 0) coop[atomicAdd(&a.cnt->coop_groups, 1u)] = g;
+            continue;
+        }
         const uint32_t b = find_block(a.boffs, a.nb, s.x);
         const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
         for (uint32_t e = l; e < s.y; e += 64)
             finish(a, boff, n, a.sa[s.x + e], s.x + e, s.x - boff, s.y, e == 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_groups_coop(RoundArgs a, const uint2 *__restrict__ groups,
+                                                     const uint32_t *__restrict__ coop)
+{
+    const uint32_t nc = a.cnt->coop_groups;
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, nt = gridDim.x * blockDim.x;
+    for (uint32_t i = 0; i < nc; ++i) {
+        const uint2 s = groups[coop[i]];
+        const uint32_t b = find_block(a.boffs, a.nb, s.x);
+        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+        for (uint32_t e = tid; e < s.y; e += nt) finish(a, boff, n, a.sa[s.x + e], s.x + e, s.x - boff, s.y, e == 0);
     }
 }
 
@@ -1924,8 +1972,11 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                    rkB);
         BMH_HIP(hipMemsetAsync(&d_cnt->next, 0, 4, c->stream));
         BMH_HIP(hipMemsetAsync(&d_cnt->dmin_bits, 0xff, 4, c->stream));
+        uint32_t *coop = (uint32_t *)c->get(WS_COOP, (size_t)ngroups * 4 + (N / kCoopGroup + 2) * 4 + 64);
+        BMH_HIP(hipMemsetAsync(&d_cnt->coop_fill, 0, 4, c->stream));
         BMH_LAUNCH(c, "bwt_group_fill", k_group_fill, std::min<uint32_t>(cdiv(ngroups, 4), 65536), 256, 0, da, dgroups,
-                   ngroups, rkA, rkB, seg_cur, d_cnt);
+                   ngroups, rkA, rkB, seg_cur, coop, d_cnt);
+        BMH_LAUNCH(c, "bwt_group_fill", k_group_fill_coop, kCoopGrid, 256, 0, da, dgroups, coop, rkA, rkB, seg_cur, d_cnt);
         read_counters();
         uint32_t ncur = h_cnt->next;
         uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
@@ -1952,7 +2003,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             a.cnt = d_cnt;
 
             BMH_HIP(hipMemsetAsync(d_cnt, 0, 8 * 4, c->stream));  // the 8 doubling-phase counters
-            BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt);
+            BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt,
+                       d_boffs, nb);
             read_counters();
 
             uint32_t nl = h_cnt->large;
@@ -1994,9 +2046,14 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 BMH_LAUNCH(c, "bwt_tiny", k_tiny, h_cnt->tiles, 256, 0, a, tiny, ntiny, prefix, tiles);
             }
             if (h_cnt->med > 0) BMH_LAUNCH(c, "bwt_medium", k_medium, h_cnt->med, kMedNT, 0, a, med);
-            if (h_cnt->groups > 0)
+            if (h_cnt->groups > 0) {
+                uint32_t *gcoop = (uint32_t *)c->get(WS_COOP, (size_t)ngroups * 4 + (N / kCoopGroup + 2) * 4 + 64) +
+                                  ngroups;  // at most N / kCoopGroup groups are that long
+                BMH_HIP(hipMemsetAsync(&d_cnt->coop_groups, 0, 4, c->stream));
                 BMH_LAUNCH(c, "bwt_groups", k_groups, std::min<uint32_t>(cdiv(h_cnt->groups, 4), 65536), 256, 0, a,
-                           groups, h_cnt->groups);
+                           groups, h_cnt->groups, gcoop);
+                BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
+            }
             read_counters();
             if (h_cnt->resolved > 0)
                 BMH_LAUNCH(c, "bwt_commit", k_commit, cdiv(h_cnt->resolved, 256), 256, 0, resolved, h_cnt->resolved,
