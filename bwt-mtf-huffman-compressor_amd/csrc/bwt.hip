@@ -54,10 +54,8 @@ constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries pe
 #endif
 constexpr uint32_t kTinyQ = BMH_TINY_Q;        // the packed tiny finish (256 segments per workgroup)
 // doubling phase
-constexpr uint32_t kTinyMax = 128;
-constexpr uint32_t kTileT = 1024;
-constexpr uint32_t kTileCap = kTileT + kTinyMax;  // 1152
-constexpr uint32_t kTileSegMax = kTileCap / 2;
+constexpr uint32_t kTinyMax = 64;     // doubling-phase segments ranked by wave shuffles (k_dtiny)
+constexpr uint32_t kDblGrid = 1024;   // fixed grid of the doubling-phase kernels (counts read on the device)
 constexpr uint32_t kMedMax = 4096;
 constexpr uint32_t kFinalFlag = 0x80000000u;
 
@@ -66,6 +64,7 @@ struct Counters {
     uint32_t lcnt[5];  // data phase: entries of each list (kListTiny .. kListGroups)
     uint32_t big, dmin_bits, flagged;
     uint32_t coop_fill, coop_groups;  // groups too long for one wave (k_group_fill / k_groups)
+    uint32_t ltiles;                  // tiles of the current large-path MSD pass (k_tiles)
 };
 constexpr uint32_t kCoopGroup = 8192;  // a group this long is walked by the whole grid
 constexpr uint32_t kCoopGrid = 1024;   // workgroups of the cooperative group kernels
@@ -1285,120 +1284,104 @@ __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 
     }
 }
 
-// ---------------------------------------------------------------- device-wide exclusive scan
-constexpr uint32_t kScanItems = 4096;  // per workgroup (1024 threads x 4)
-
-__global__ __launch_bounds__(1024) void k_scan_reduce(const uint32_t *__restrict__ in, uint32_t stride, uint32_t count,
-                                                      uint32_t *__restrict__ partials)
+// Tiles of <= kDTile slots over a segment list whose length is on the device: one workgroup
+// scans the tile counts (1024 segments per step) and writes tiles[] (seg, start, len),
+// segtiles[s] = {first tile, tile count} and *ntiles. S: {gstart, len, ...} in its first two
+// words (Seg4, LSeg). With `orv`/`mnv`, the per-segment OR / minimum accumulators of the data
+// phase's MSD pass are reset too.
+template <class S, class T>
+__global__ __launch_bounds__(1024) void k_tiles(const S *__restrict__ segs, const uint32_t *__restrict__ nseg_p,
+                                                T *__restrict__ tiles, uint2 *__restrict__ segtiles,
+                                                uint32_t *__restrict__ ntiles, unsigned long long *__restrict__ orv,
+                                                unsigned long long *__restrict__ mnv)
 {
     __shared__ uint32_t s_tmp[17];
-    const uint32_t base = blockIdx.x * kScanItems + threadIdx.x * 4;
-    uint32_t s = 0;
-    for (int i = 0; i < 4; ++i)
-        if (base + i < count) s += in[(size_t)(base + i) * stride];
-    uint32_t total;
-    block_excl_sum<1024>(s, s_tmp, &total);
-    if (threadIdx.x == 0) partials[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(1024) void k_scan_partials(uint32_t *__restrict__ partials, uint32_t n)
-{
-    __shared__ uint32_t s_tmp[17];
+    const uint32_t nseg = *nseg_p;
     uint32_t carry = 0;
-    for (uint32_t base = 0; base < n; base += 1024) {
+    for (uint32_t base = 0; base < nseg; base += 1024) {
         const uint32_t i = base + threadIdx.x;
-        const uint32_t v = i < n ? partials[i] : 0u;
+        uint32_t st = 0, ln = 0, nt = 0;
+        if (i < nseg) {
+            const uint32_t *w = (const uint32_t *)&segs[i];
+            st = w[0];
+            ln = w[1];
+            nt = (ln + kDTile - 1) / kDTile;
+        }
         uint32_t total;
-        const uint32_t ex = block_excl_sum<1024>(v, s_tmp, &total);
-        if (i < n) partials[i] = carry + ex;
+        const uint32_t ex = carry + block_excl_sum<1024>(nt, s_tmp, &total);
+        if (i < nseg) {
+            segtiles[i] = make_uint2(ex, nt);
+            for (uint32_t j = 0; j < nt; ++j) {
+                T t;
+                t.seg = i;
+                t.start = st + j * kDTile;
+                t.len = min(kDTile, ln - j * kDTile);
+                t.pad = 0;
+                tiles[ex + j] = t;
+            }
+            if (orv) orv[i] = 0;
+            if (mnv) mnv[i] = ~0ull;
+        }
         carry += total;
     }
+    if (threadIdx.x == 0) *ntiles = carry;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_down(const uint32_t *__restrict__ in, uint32_t stride, uint32_t count,
-                                                    const uint32_t *__restrict__ partials, uint32_t *__restrict__ out)
+// Doubling-phase segments of <= kTinyMax (64) rotations, packed like k_finish_tiny: each wave
+// takes 64 consecutive list entries and lays their rotations side by side over its lanes in
+// rounds of <= 64; each rotation's new slot = segment start + #(keys < mine) + #(equal keys
+// before me), by wave shuffles; group = equal keys. Grid-stride over the list (count on the
+// device).
+__global__ __launch_bounds__(256) void k_dtiny(RoundArgs a, const uint2 *__restrict__ tiny)
 {
-    __shared__ uint32_t s_tmp[17];
-    const uint32_t base = blockIdx.x * kScanItems + threadIdx.x * 4;
-    uint32_t v[4], s = 0;
-    for (int i = 0; i < 4; ++i) {
-        v[i] = base + i < count ? in[(size_t)(base + i) * stride] : 0u;
-        s += v[i];
-    }
-    uint32_t ex = block_excl_sum<1024>(s, s_tmp, nullptr) + partials[blockIdx.x];
-    for (int i = 0; i < 4; ++i) {
-        if (base + i < count) out[base + i] = ex;
-        ex += v[i];
-    }
-}
-
-__global__ void k_tile_heads(const uint32_t *__restrict__ prefix, uint32_t n, uint32_t *__restrict__ tiles,
-                             Counters *cnt)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t t = prefix[i] / kTileT;
-    if (i == 0 || prefix[i - 1] / kTileT != t) tiles[wave_append(&cnt->tiles)] = i;
-}
-
-// One workgroup per tile of consecutive tiny segments (<= 1152 elements). Each element's new
-// slot = segment start + #(keys < mine) + #(equal keys before me); group = equal keys.
-__global__ __launch_bounds__(256) void k_tiny(RoundArgs a, const uint2 *__restrict__ tiny, uint32_t ntiny,
-                                              const uint32_t *__restrict__ prefix, const uint32_t *__restrict__ tiles)
-{
-    __shared__ uint32_t s_key[kTileCap], s_pos[kTileCap];
-    __shared__ uint16_t s_seg[kTileCap];
-    __shared__ uint32_t s_gstart[kTileSegMax], s_lstart[kTileSegMax], s_len[kTileSegMax], s_boff[kTileSegMax],
-        s_n[kTileSegMax];
-    const uint32_t head = tiles[blockIdx.x];
-    const uint32_t base = prefix[head];
-    const uint32_t t = base / kTileT;
-    uint32_t nseg = 0;
-    for (uint32_t w = 0;; w += 256) {
-        const uint32_t i = head + w + threadIdx.x;
-        const bool in = i < ntiny && prefix[i] / kTileT == t;
-        const uint32_t c = __syncthreads_count(in);
-        nseg += c;
-        if (c < 256) break;
-    }
-    for (uint32_t k = threadIdx.x; k < nseg; k += 256) {
-        const uint2 s = tiny[head + k];
-        const uint32_t b = find_block(a.boffs, a.nb, s.x);
-        s_gstart[k] = s.x;
-        s_len[k] = s.y;
-        s_lstart[k] = prefix[head + k] - base;
-        s_boff[k] = a.boffs[b];
-        s_n[k] = a.boffs[b + 1] - a.boffs[b];
-    }
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nseg; k += 256)
-        for (uint32_t e = s_lstart[k], e1 = e + s_len[k]; e < e1; ++e) s_seg[e] = (uint16_t)k;
-    const uint32_t total = s_lstart[nseg - 1] + s_len[nseg - 1];
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < total; e += 256) {
-        const uint32_t k = s_seg[e];
-        const uint32_t p = a.sa[s_gstart[k] + (e - s_lstart[k])];
-        s_pos[e] = p;
-        s_key[e] = round_key(a, s_boff[k], s_n[k], p);
-    }
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < total; e += 256) {
-        const uint32_t k = s_seg[e];
-        const uint32_t l0 = s_lstart[k], m = s_len[k];
-        const uint32_t ke = s_key[e];
-        uint32_t lt = 0, eqb = 0, eqt = 0;
-        for (uint32_t f = l0; f < l0 + m; ++f) {
-            const uint32_t kf = s_key[f];
-            lt += kf < ke;
-            const bool eq = kf == ke;
-            eqt += eq;
-            eqb += eq && f < e;
+    const uint32_t ntiny = a.cnt->tiny;
+    const uint32_t l = threadIdx.x & 63u;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nwaves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t i0 = wave * 64; i0 < ntiny; i0 += nwaves * 64) {  // wave-uniform
+        const uint2 sgl = i0 + l < ntiny ? tiny[i0 + l] : make_uint2(0, 0);
+        const uint32_t incl = wave_incl_sum(sgl.y), st = incl - sgl.y;
+        const uint32_t total = __shfl(incl, 63, 64);
+        for (uint32_t base = 0; base < total;) {  // wave-uniform rounds
+            const bool in = sgl.y > 0 && st >= base && incl <= base + 64;
+            const uint64_t inm = __ballot(in), afterm = __ballot(sgl.y > 0 && st >= base && incl > base + 64);
+            const uint32_t s0 = (uint32_t)__ffsll((unsigned long long)inm) - 1;
+            const uint32_t nbase = afterm ? (uint32_t)__shfl((int)st, __ffsll((unsigned long long)afterm) - 1, 64) : total;
+            uint64_t B = in ? 1ull << (st - base) : 0ull;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) B |= __shfl_xor(B, off, 64);
+            const bool live = l < nbase - base;
+            const uint64_t below = l == 63 ? B : B & ((2ull << l) - 1);
+            const uint32_t pos = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+            const uint32_t sl = s0 + (uint32_t)__builtin_popcountll(B & ((1ull << pos) - 1));
+            const uint32_t gstart = __shfl((int)sgl.x, (int)sl, 64), slen = __shfl((int)sgl.y, (int)sl, 64);
+            const uint32_t len = slen * (uint32_t)live;
+            const uint32_t idx = l - pos;
+            uint32_t p = 0, boff = 0, n = 1, key = 0xffffffffu;
+            if (live) {
+                const uint32_t b = find_block(a.boffs, a.nb, gstart);
+                boff = a.boffs[b];
+                n = a.boffs[b + 1] - boff;
+                p = a.sa[gstart + idx];
+                key = round_key(a, boff, n, p);
+            }
+            uint32_t mx = len;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+            uint32_t lt = 0, eqb = 0, eqt = 0;
+            for (uint32_t j = 0; j < mx; ++j) {  // every lane takes part in the shuffles
+                const uint32_t kj = __shfl(key, (int)min(pos + j, 63u), 64);
+                const bool m = j < len;
+                lt += m && kj < key;
+                eqt += m && kj == key;
+                eqb += m && kj == key && j < idx;
+            }
+            if (live) {
+                const uint32_t slot = gstart + lt + eqb;
+                a.sa[slot] = p;
+                finish(a, boff, n, p, slot, gstart - boff + lt, eqt, eqb == 0);
+            }
+            base = nbase;
         }
-        const uint32_t p = s_pos[e];
-        const uint32_t slot = s_gstart[k] + lt + eqb;
-        a.sa[slot] = p;
-        const uint32_t boff = s_boff[k];
-        finish(a, boff, s_n[k], p, slot, s_gstart[k] - boff + lt, eqt, eqb == 0);
     }
 }
 
@@ -1406,13 +1389,26 @@ __global__ __launch_bounds__(256) void k_tiny(RoundArgs a, const uint2 *__restri
 // digits skipped) in LDS, then equal-key groups via block max / suffix-min scans.
 constexpr int kMedNT = 256, kMedIPT = kMedMax / kMedNT;
 
+__device__ __forceinline__ void medium_one(const RoundArgs &a, const uint2 sg, uint32_t (&s_k)[2][kMedMax],
+                                           uint32_t (&s_v)[2][kMedMax], uint16_t (&s_cnt)[16 * kMedNT],
+                                           uint32_t (&s_tmp)[8], uint32_t &s_or, uint32_t &s_and);
 __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__restrict__ med)
 {
     __shared__ uint32_t s_k[2][kMedMax], s_v[2][kMedMax];
     __shared__ uint16_t s_cnt[16 * kMedNT];
     __shared__ uint32_t s_tmp[8];
     __shared__ uint32_t s_or, s_and;
-    const uint2 sg = med[blockIdx.x];
+    const uint32_t nmed = a.cnt->med;
+    for (uint32_t it = blockIdx.x; it < nmed; it += gridDim.x) {
+        medium_one(a, med[it], s_k, s_v, s_cnt, s_tmp, s_or, s_and);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void medium_one(const RoundArgs &a, const uint2 sg, uint32_t (&s_k)[2][kMedMax],
+                                           uint32_t (&s_v)[2][kMedMax], uint16_t (&s_cnt)[16 * kMedNT],
+                                           uint32_t (&s_tmp)[8], uint32_t &s_or, uint32_t &s_and)
+{
     const uint32_t b = find_block(a.boffs, a.nb, sg.x);
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint32_t m = sg.y;
@@ -1497,35 +1493,40 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
     }
 }
 
-// Large segments of the doubling phase: global MSD passes on the 32-bit rank key.
+// Large segments of the doubling phase: global MSD passes on the 32-bit rank key, 8 bits per
+// pass, grid-stride over tiles / segments whose counts k_tiles left on the device.
 __global__ __launch_bounds__(256) void k_lhist(RoundArgs a, const LSeg *__restrict__ lsegs,
                                                const LTile *__restrict__ tiles, uint32_t *__restrict__ key,
                                                uint32_t *__restrict__ thist)
 {
     __shared__ uint32_t h[256];
-    const LTile t = tiles[blockIdx.x];
-    const LSeg s = lsegs[t.seg];
-    const uint32_t b = find_block(a.boffs, a.nb, s.gstart);
-    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
-        const uint32_t j = t.start + e;
-        uint32_t k;
-        if (s.gathered) {
-            k = key[j];
-        } else {
-            k = round_key(a, boff, n, a.sa[j]);
-            key[j] = k;
+    const uint32_t ntl = a.cnt->ltiles;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        const LTile t = tiles[tb];
+        const LSeg s = lsegs[t.seg];
+        const uint32_t b = find_block(a.boffs, a.nb, s.gstart);
+        const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+            const uint32_t j = t.start + e;
+            uint32_t k;
+            if (s.gathered) {
+                k = key[j];
+            } else {
+                k = round_key(a, boff, n, a.sa[j]);
+                key[j] = k;
+            }
+            atomicAdd(&h[(k >> s.shift) & 255u], 1u);
         }
-        atomicAdd(&h[(k >> s.shift) & 255u], 1u);
+        __syncthreads();
+        thist[(size_t)tb * 256 + threadIdx.x] = h[threadIdx.x];
+        __syncthreads();
     }
-    __syncthreads();
-    thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
 __device__ __forceinline__ void push_sub(uint32_t gstart, uint32_t len, uint32_t shift, uint2 *tiny, uint2 *med,
-                                         LSeg *large_next, uint2 *groups, Counters *cnt)
+                                         LSeg *large_next, uint32_t *large_next_cnt, uint2 *groups, Counters *cnt)
 {
     if (len == 1) {
         groups[wave_append(&cnt->groups)] = make_uint2(gstart, len);
@@ -1539,79 +1540,92 @@ __device__ __forceinline__ void push_sub(uint32_t gstart, uint32_t len, uint32_t
         l.len = len;
         l.shift = shift - 8;
         l.gathered = 1;
-        large_next[wave_append(&cnt->large_next)] = l;
+        large_next[wave_append(large_next_cnt)] = l;
     } else {
         groups[wave_append(&cnt->groups)] = make_uint2(gstart, len);  // keys exhausted: equal
     }
 }
 
-__global__ __launch_bounds__(256) void k_lscan(const LSeg *__restrict__ lsegs, const uint2 *__restrict__ segtiles,
-                                               uint32_t *__restrict__ thist, uint32_t *__restrict__ nomove,
-                                               uint2 *tiny, uint2 *med, LSeg *large_next, uint2 *groups, Counters *cnt)
+__global__ __launch_bounds__(256) void k_lscan(const LSeg *__restrict__ lsegs, const uint32_t *__restrict__ nseg_p,
+                                               const uint2 *__restrict__ segtiles, uint32_t *__restrict__ thist,
+                                               uint32_t *__restrict__ nomove, uint2 *tiny, uint2 *med, LSeg *large_next,
+                                               uint32_t *large_next_cnt, uint2 *groups, Counters *cnt)
 {
     __shared__ uint32_t s_tmp[8];
-    const LSeg s = lsegs[blockIdx.x];
-    const uint2 tr = segtiles[blockIdx.x];
+    const uint32_t nseg = *nseg_p;
     const uint32_t d = threadIdx.x;
-    uint32_t run = 0;
-    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
-        const uint32_t v = thist[(size_t)t * 256 + d];
-        thist[(size_t)t * 256 + d] = run;
-        run += v;
-    }
-    const uint32_t tot = run;
-    const int nz = __syncthreads_count(tot > 0);
-    const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
-    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.gstart + base;
-    if (nz == 1) {
-        if (d == 0) {
-            nomove[blockIdx.x] = 1;
-            push_sub(s.gstart, s.len, s.shift, tiny, med, large_next, groups, cnt);
+    for (uint32_t sgi = blockIdx.x; sgi < nseg; sgi += gridDim.x) {
+        const LSeg s = lsegs[sgi];
+        const uint2 tr = segtiles[sgi];
+        uint32_t run = 0;
+        for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
+            const uint32_t v = thist[(size_t)t * 256 + d];
+            thist[(size_t)t * 256 + d] = run;
+            run += v;
         }
-    } else {
-        if (d == 0) nomove[blockIdx.x] = 0;
-        if (tot > 0) push_sub(s.gstart + base, tot, s.shift, tiny, med, large_next, groups, cnt);
+        const uint32_t tot = run;
+        const int nz = __syncthreads_count(tot > 0);
+        const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
+        for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.gstart + base;
+        if (nz == 1) {
+            if (d == 0) {
+                nomove[sgi] = 1;
+                push_sub(s.gstart, s.len, s.shift, tiny, med, large_next, large_next_cnt, groups, cnt);
+            }
+        } else {
+            if (d == 0) nomove[sgi] = 0;
+            if (tot > 0) push_sub(s.gstart + base, tot, s.shift, tiny, med, large_next, large_next_cnt, groups, cnt);
+        }
     }
 }
 
 __global__ __launch_bounds__(256) void k_lscatter(const LSeg *__restrict__ lsegs, const LTile *__restrict__ tiles,
-                                                  const uint32_t *__restrict__ nomove, const uint32_t *__restrict__ thist,
-                                                  const uint32_t *__restrict__ sa, const uint32_t *__restrict__ key,
-                                                  uint32_t *__restrict__ sa2, uint32_t *__restrict__ key2)
+                                                  const uint32_t *__restrict__ ntl_p, const uint32_t *__restrict__ nomove,
+                                                  const uint32_t *__restrict__ thist, const uint32_t *__restrict__ sa,
+                                                  const uint32_t *__restrict__ key, uint32_t *__restrict__ sa2,
+                                                  uint32_t *__restrict__ key2)
 {
     __shared__ uint32_t cur[256];
-    const LTile t = tiles[blockIdx.x];
-    if (nomove[t.seg]) return;
-    const uint32_t shift = lsegs[t.seg].shift;
-    cur[threadIdx.x] = thist[(size_t)blockIdx.x * 256 + threadIdx.x];
-    __syncthreads();
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
-        const uint32_t j = t.start + e;
-        const uint32_t k = key[j];
-        const uint32_t slot = atomicAdd(&cur[(k >> shift) & 255u], 1u);
-        sa2[slot] = sa[j];
-        key2[slot] = k;
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        const LTile t = tiles[tb];
+        if (nomove[t.seg]) continue;  // workgroup-uniform
+        const uint32_t shift = lsegs[t.seg].shift;
+        cur[threadIdx.x] = thist[(size_t)tb * 256 + threadIdx.x];
+        __syncthreads();
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+            const uint32_t j = t.start + e;
+            const uint32_t k = key[j];
+            const uint32_t slot = atomicAdd(&cur[(k >> shift) & 255u], 1u);
+            sa2[slot] = sa[j];
+            key2[slot] = k;
+        }
+        __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(256) void k_lcopy(const LTile *__restrict__ tiles, const uint32_t *__restrict__ nomove,
-                                               uint32_t *__restrict__ sa, uint32_t *__restrict__ key,
-                                               const uint32_t *__restrict__ sa2, const uint32_t *__restrict__ key2)
+__global__ __launch_bounds__(256) void k_lcopy(const LTile *__restrict__ tiles, const uint32_t *__restrict__ ntl_p,
+                                               const uint32_t *__restrict__ nomove, uint32_t *__restrict__ sa,
+                                               uint32_t *__restrict__ key, const uint32_t *__restrict__ sa2,
+                                               const uint32_t *__restrict__ key2)
 {
-    const LTile t = tiles[blockIdx.x];
-    if (nomove[t.seg]) return;
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
-        const uint32_t j = t.start + e;
-        sa[j] = sa2[j];
-        key[j] = key2[j];
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        const LTile t = tiles[tb];
+        if (nomove[t.seg]) continue;
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+            const uint32_t j = t.start + e;
+            sa[j] = sa2[j];
+            key[j] = key2[j];
+        }
     }
 }
 
 // Groups produced by the large path (singletons, or key-exhausted equal-key groups). One wave
 // per group; groups longer than kCoopGroup go to `coop` for k_groups_coop (the whole grid).
-__global__ __launch_bounds__(256) void k_groups(RoundArgs a, const uint2 *__restrict__ groups, uint32_t ng,
-                                                uint32_t *__restrict__ coop)
+__global__ __launch_bounds__(256) void k_groups(RoundArgs a, const uint2 *__restrict__ groups, uint32_t *__restrict__ coop)
 {
+    const uint32_t ng = a.cnt->groups;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t l = threadIdx.x & 63u;
@@ -1641,11 +1655,12 @@ __global__ __launch_bounds__(256) void k_groups_coop(RoundArgs a, const uint2 *_
     }
 }
 
-__global__ void k_commit(const uint32_t *__restrict__ list, uint32_t cnt, const uint32_t *__restrict__ src,
-                         uint32_t *__restrict__ dst)
+__global__ void k_commit(const uint32_t *__restrict__ list, const uint32_t *__restrict__ cnt_p,
+                         const uint32_t *__restrict__ src, uint32_t *__restrict__ dst)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < cnt) dst[list[i]] = src[list[i]];
+    const uint32_t cnt = *cnt_p;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x)
+        dst[list[i]] = src[list[i]];
 }
 
 __global__ void k_fill_u32(uint32_t *p, uint32_t v, uint32_t n)
@@ -1963,10 +1978,18 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         LSeg *large = (LSeg *)c->get(WS_DLARGE, lcap * sizeof(LSeg));
         LSeg *large2 = (LSeg *)c->get(WS_DLARGE2, lcap * sizeof(LSeg));
         uint2 *groups = (uint2 *)c->get(WS_DGROUPS, (N + 2) * 8);
-        uint32_t *prefix = (uint32_t *)c->get(WS_PREFIX, seg_cap * 4);
-        uint32_t *partials = (uint32_t *)c->get(WS_SCAN_PART, (seg_cap / kScanItems + 2) * 4);
-        uint32_t *tiles = (uint32_t *)c->get(WS_TILES, seg_cap * 4);
         uint32_t *resolved = (uint32_t *)c->get(WS_RESOLVED, N * 4);
+        // large-path tiles, bounded by the slots over kDTile plus one partial tile per segment
+        const size_t tcap = N / kDTile + lcap + 2;
+        uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, tcap * sizeof(LTile) + lcap * 12 + 64);
+        LTile *d_ltiles = (LTile *)d_lt;
+        uint2 *d_lsegtiles = (uint2 *)(d_lt + tcap * sizeof(LTile));
+        uint32_t *d_lnomove = (uint32_t *)(d_lt + tcap * sizeof(LTile) + lcap * 8);
+        uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, tcap * 256 * 4);
+        uint32_t *gcoop = (uint32_t *)c->get(WS_COOP, (size_t)ngroups * 4 + (N / kCoopGroup + 2) * 4 + 64) + ngroups;
+        // MSD passes per round: ranks are block-local (< n), the first pass takes their highest
+        // nonzero byte (k_classify), 8 bits per pass
+        const uint32_t npass = bt.max_n > (1u << 24) ? 4u : bt.max_n > (1u << 16) ? 3u : bt.max_n > 256u ? 2u : 1u;
 
         BMH_LAUNCH(c, "bwt_rank_fill", k_rank_fill, dim3(cdiv(bt.max_n, 4096), nb), 256, 0, d_boffs, bflag, sa, rkA,
                    rkB);
@@ -1981,9 +2004,9 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         uint32_t ncur = h_cnt->next;
         uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
         int round = 0;
-        std::vector<LSeg> hl;
-        std::vector<LTile> hlt;
-        std::vector<uint2> hlst;
+        // One host wait per round (the next round's segment count and termination): every
+        // kernel of a round reads its list lengths from the device counters and strides over
+        // them with a fixed grid; the large path's tiles are built on the device (k_tiles).
         while (ncur > 0) {
             if (D == 0) fail(BMH_EHIP, "bwt: internal error (zero doubling depth)");
             RoundArgs a;
@@ -2003,61 +2026,31 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             a.cnt = d_cnt;
 
             BMH_HIP(hipMemsetAsync(d_cnt, 0, 8 * 4, c->stream));  // the 8 doubling-phase counters
+            BMH_HIP(hipMemsetAsync(&d_cnt->coop_groups, 0, 4, c->stream));
             BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt,
                        d_boffs, nb);
-            read_counters();
-
-            uint32_t nl = h_cnt->large;
-            LSeg *lcur = large, *lnxt = large2;
-            while (nl > 0) {
-                hl.resize(nl);
-                c->d2h(hl.data(), lcur, nl * sizeof(LSeg));
-                c->sync();
-                build_tiles<LSeg, LTile>(hl, kDTile, hlt, hlst, [](const LSeg &s) { return s.gstart; },
-                                         [](const LSeg &s) { return s.len; });
-                const uint32_t ntl = (uint32_t)hlt.size();
-                uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(LTile) + nl * 8 + nl * 4 + 64);
-                LTile *d_tiles = (LTile *)d_lt;
-                uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(LTile));
-                uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(LTile) + nl * 8);
-                c->h2d(d_tiles, hlt.data(), ntl * sizeof(LTile));
-                c->h2d(d_segtiles, hlst.data(), nl * 8);
-                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
-                BMH_HIP(hipMemsetAsync(&d_cnt->large_next, 0, 4, c->stream));
-                BMH_LAUNCH(c, "bwt_lhist", k_lhist, ntl, 256, 0, a, lcur, d_tiles, key, thist);
-                BMH_LAUNCH(c, "bwt_lscan", k_lscan, nl, 256, 0, lcur, d_segtiles, thist, d_nomove, tiny, med, lnxt,
-                           groups, d_cnt);
-                BMH_LAUNCH(c, "bwt_lscatter", k_lscatter, ntl, 256, 0, lcur, d_tiles, d_nomove, thist, sa, key, sa2,
+            for (uint32_t pass = 0; pass < npass; ++pass) {  // passes with no segments exit at once
+                uint32_t *cnt_in = pass & 1 ? &d_cnt->large_next : &d_cnt->large;
+                uint32_t *cnt_out = pass & 1 ? &d_cnt->large : &d_cnt->large_next;
+                LSeg *lin = pass & 1 ? large2 : large, *lout = pass & 1 ? large : large2;
+                BMH_HIP(hipMemsetAsync(cnt_out, 0, 4, c->stream));
+                BMH_LAUNCH(c, "bwt_ltiles", (k_tiles<LSeg, LTile>), 1, 1024, 0, lin, cnt_in, d_ltiles, d_lsegtiles,
+                           &d_cnt->ltiles, nullptr, nullptr);
+                BMH_LAUNCH(c, "bwt_lhist", k_lhist, kDblGrid, 256, 0, a, lin, d_ltiles, key, thist);
+                BMH_LAUNCH(c, "bwt_lscan", k_lscan, kDblGrid, 256, 0, lin, cnt_in, d_lsegtiles, thist, d_lnomove, tiny, med,
+                           lout, cnt_out, groups, d_cnt);
+                BMH_LAUNCH(c, "bwt_lscatter", k_lscatter, kDblGrid, 256, 0, lin, d_ltiles, &d_cnt->ltiles, d_lnomove, thist,
+                           sa, key, sa2, key2);
+                BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, kDblGrid, 256, 0, d_ltiles, &d_cnt->ltiles, d_lnomove, sa, key, sa2,
                            key2);
-                BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, ntl, 256, 0, d_tiles, d_nomove, sa, key, sa2, key2);
-                read_counters();
-                nl = h_cnt->large_next;
-                std::swap(lcur, lnxt);
             }
-
-            const uint32_t ntiny = h_cnt->tiny;
-            if (ntiny > 0) {
-                const uint32_t nparts = cdiv(ntiny, kScanItems);
-                BMH_LAUNCH(c, "bwt_scan_reduce", k_scan_reduce, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials);
-                BMH_LAUNCH(c, "bwt_scan_partials", k_scan_partials, 1, 1024, 0, partials, nparts);
-                BMH_LAUNCH(c, "bwt_scan_down", k_scan_down, nparts, 1024, 0, &tiny[0].y, 2u, ntiny, partials, prefix);
-                BMH_LAUNCH(c, "bwt_tile_heads", k_tile_heads, cdiv(ntiny, 256), 256, 0, prefix, ntiny, tiles, d_cnt);
-                read_counters();
-                BMH_LAUNCH(c, "bwt_tiny", k_tiny, h_cnt->tiles, 256, 0, a, tiny, ntiny, prefix, tiles);
-            }
-            if (h_cnt->med > 0) BMH_LAUNCH(c, "bwt_medium", k_medium, h_cnt->med, kMedNT, 0, a, med);
-            if (h_cnt->groups > 0) {
-                uint32_t *gcoop = (uint32_t *)c->get(WS_COOP, (size_t)ngroups * 4 + (N / kCoopGroup + 2) * 4 + 64) +
-                                  ngroups;  // at most N / kCoopGroup groups are that long
-                BMH_HIP(hipMemsetAsync(&d_cnt->coop_groups, 0, 4, c->stream));
-                BMH_LAUNCH(c, "bwt_groups", k_groups, std::min<uint32_t>(cdiv(h_cnt->groups, 4), 65536), 256, 0, a,
-                           groups, h_cnt->groups, gcoop);
-                BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
-            }
+            BMH_LAUNCH(c, "bwt_tiny", k_dtiny, kDblGrid, 256, 0, a, tiny);
+            BMH_LAUNCH(c, "bwt_medium", k_medium, kDblGrid, kMedNT, 0, a, med);
+            BMH_LAUNCH(c, "bwt_groups", k_groups, kDblGrid, 256, 0, a, groups, gcoop);
+            BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
+            BMH_LAUNCH(c, "bwt_commit", k_commit, kDblGrid, 256, 0, resolved, &d_cnt->resolved, a.rk_nxt,
+                       (uint32_t *)a.rk_cur);
             read_counters();
-            if (h_cnt->resolved > 0)
-                BMH_LAUNCH(c, "bwt_commit", k_commit, cdiv(h_cnt->resolved, 256), 256, 0, resolved, h_cnt->resolved,
-                           a.rk_nxt, (uint32_t *)a.rk_cur);
             ncur = h_cnt->next;
             std::swap(seg_cur, seg_nxt);
             D = a.newD;
