@@ -61,8 +61,10 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t lcnt[5];  // data phase: entries of each list (kListTiny .. kListGroups)
-    uint32_t big, dmin_bits, flagged;
+    uint32_t lc[2][4];  // data phase: entries of the tiny / fin / finb / big lists of each parity
+    uint32_t lgroups;   // data phase: entries of the groups list (grows over the whole phase)
+    uint32_t dtiles;    // tiles of the current MSD pass (k_tiles)
+    uint32_t dmin_bits, flagged;
     uint32_t coop_fill, coop_groups;  // groups too long for one wave (k_group_fill / k_groups)
     uint32_t ltiles;                  // tiles of the current large-path MSD pass (k_tiles)
 };
@@ -91,7 +93,8 @@ struct DataArgs {
     uint8_t *L;
     uint32_t *prim;
     uint32_t *bflag;   // block keeps tied groups -> needs the rank phase
-    Seg4 *const *lists;  // device table: the list each deferral class appends to (kList*)
+    Seg4 *lists[5];      // the list each deferral class appends to (kList*)
+    uint32_t *lcnt;      // their counters (cnt->lc[parity]; groups: cnt->lgroups)
     Counters *cnt;
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
 };
@@ -141,7 +144,10 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
 // The first four are refilled every round; the groups list grows over the whole data phase.
 enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListBig = 3, kListGroups = 4, kNumLists = 5 };
 
-__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l) { return &a.cnt->lcnt[l]; }
+__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l)
+{
+    return l == 4u ? &a.cnt->lgroups : &a.lcnt[l];
+}
 __device__ __forceinline__ Seg4 *list_base(const DataArgs &a, uint32_t l) { return a.lists[l]; }
 
 // A tied run of m rotations, grouped up to bit depth nd (sg = {gs, m, nd, b}): another finish
@@ -365,9 +371,9 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     }
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
     if (run > kBigCap)
-        big[wave_append(&cnt->big)] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        big[wave_append(&cnt->lc[0][kListBig])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[wave_append(&cnt->lcnt[kListFinb])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        fin[wave_append(&cnt->lc[0][kListFinb])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -670,86 +676,90 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 // splits across rounds); each rotation is ranked inside its segment by the next 64 rotation
 // bits with wave shuffles. Tie groups of 2-5 rotations are the common case on text, so a wave
 // per segment would leave most lanes idle.
-__global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list, uint32_t nlist)
+__global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list,
+                                                     const uint32_t *__restrict__ nlist_p)
 {
     __shared__ DeferQueue<kTinyQ> dq;
-    dq_init(dq);
-    __syncthreads();
+    const uint32_t nlist = *nlist_p;
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
-    const uint32_t i0 = (blockIdx.x * 4 + w) * 64;
-    if (i0 < nlist) {  // wave-uniform
-        const Seg4 sgl = i0 + l < nlist ? list[i0 + l] : make_uint4(0, 0, 0, 0);
-        const uint32_t incl = wave_incl_sum(sgl.y), st = incl - sgl.y;
-        const uint32_t total = __shfl(incl, 63, 64);
-        for (uint32_t base = 0; base < total;) {  // wave-uniform rounds
-            // the round: the run of segments from `base` that fits in 64 lanes
-            const bool in = sgl.y > 0 && st >= base && incl <= base + 64;
-            const uint64_t inm = __ballot(in), afterm = __ballot(sgl.y > 0 && st >= base && incl > base + 64);
-            const uint32_t s0 = (uint32_t)__ffsll((unsigned long long)inm) - 1;
-            const uint32_t nbase = afterm ? (uint32_t)__shfl((int)st, __ffsll((unsigned long long)afterm) - 1, 64) : total;
-            uint64_t B = in ? 1ull << (st - base) : 0ull;  // segment starts inside the round
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) B |= __shfl_xor(B, off, 64);
-            const bool live = l < nbase - base;
-            const uint64_t below = l == 63 ? B : B & ((2ull << l) - 1);
-            const uint32_t pos = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;  // my segment's first lane
-            const uint32_t sl = s0 + (uint32_t)__builtin_popcountll(B & ((1ull << pos) - 1));
-            // (shuffles with the whole wave active: a source lane may be past this round)
-            const uint32_t gstart = __shfl((int)sgl.x, (int)sl, 64), slen = __shfl((int)sgl.y, (int)sl, 64);
-            const uint32_t db = __shfl((int)sgl.z, (int)sl, 64), b = __shfl((int)sgl.w, (int)sl, 64);
-            const uint32_t len = slen * (uint32_t)live;
-            const uint32_t idx = l - pos;
-            uint32_t p = 0, boff = 0, n = 1;
-            uint64_t key = ~0ull;
-            const uint8_t *blk = a.data;
-            if (live) {
-                boff = a.boffs[b];
-                n = a.boffs[b + 1] - boff;
-                blk = a.data + boff;
-                p = a.sa[gstart + idx];
-                key = rot_window(blk, n, p, db);
-            }
-            uint32_t mx = len;
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-            uint32_t lt = 0, eqb = 0, eqt = 0;
-            for (uint32_t j = 0; j < mx; ++j) {  // every lane takes part in the shuffles
-                const int src = (int)min(pos + j, 63u);
-                const uint32_t klo = __shfl((uint32_t)key, src, 64), khi = __shfl((uint32_t)(key >> 32), src, 64);
-                const uint64_t kj = ((uint64_t)khi << 32) | klo;
-                const bool m = j < len;
-                lt += m && kj < key;
-                eqt += m && kj == key;
-                eqb += m && kj == key && j < idx;
-            }
-            if (live) {
-                const uint64_t newbits = (uint64_t)db + 64;
-                const bool final_depth = newbits >= 8ull * n;
-                const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
-                if (eqt > 1 && eqb == 0)
-                    dq_push(a, dq, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
-                a.sa[slot] = p;
-                if (eqt == 1 || final_depth) {
-                    a.L[slot] = lastcol_byte(blk, n, p);
-                    if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+    {
+        const uint32_t g0 = blockIdx.x * 256;  // the workgroup's 256 entries (exact grid)
+        dq_init(dq);
+        __syncthreads();
+        const uint32_t i0 = g0 + w * 64;
+        if (i0 < nlist) {  // wave-uniform
+            const Seg4 sgl = i0 + l < nlist ? list[i0 + l] : make_uint4(0, 0, 0, 0);
+            const uint32_t incl = wave_incl_sum(sgl.y), st = incl - sgl.y;
+            const uint32_t total = __shfl(incl, 63, 64);
+            for (uint32_t base = 0; base < total;) {  // wave-uniform rounds
+                // the round: the run of segments from `base` that fits in 64 lanes
+                const bool in = sgl.y > 0 && st >= base && incl <= base + 64;
+                const uint64_t inm = __ballot(in), afterm = __ballot(sgl.y > 0 && st >= base && incl > base + 64);
+                const uint32_t s0 = (uint32_t)__ffsll((unsigned long long)inm) - 1;
+                const uint32_t nbase = afterm ? (uint32_t)__shfl((int)st, __ffsll((unsigned long long)afterm) - 1, 64) : total;
+                uint64_t B = in ? 1ull << (st - base) : 0ull;  // segment starts inside the round
+    #pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) B |= __shfl_xor(B, off, 64);
+                const bool live = l < nbase - base;
+                const uint64_t below = l == 63 ? B : B & ((2ull << l) - 1);
+                const uint32_t pos = live ? 63u - (uint32_t)__builtin_clzll(below) : 0u;  // my segment's first lane
+                const uint32_t sl = s0 + (uint32_t)__builtin_popcountll(B & ((1ull << pos) - 1));
+                // (shuffles with the whole wave active: a source lane may be past this round)
+                const uint32_t gstart = __shfl((int)sgl.x, (int)sl, 64), slen = __shfl((int)sgl.y, (int)sl, 64);
+                const uint32_t db = __shfl((int)sgl.z, (int)sl, 64), b = __shfl((int)sgl.w, (int)sl, 64);
+                const uint32_t len = slen * (uint32_t)live;
+                const uint32_t idx = l - pos;
+                uint32_t p = 0, boff = 0, n = 1;
+                uint64_t key = ~0ull;
+                const uint8_t *blk = a.data;
+                if (live) {
+                    boff = a.boffs[b];
+                    n = a.boffs[b + 1] - boff;
+                    blk = a.data + boff;
+                    p = a.sa[gstart + idx];
+                    key = rot_window(blk, n, p, db);
                 }
+                uint32_t mx = len;
+    #pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+                uint32_t lt = 0, eqb = 0, eqt = 0;
+                for (uint32_t j = 0; j < mx; ++j) {  // every lane takes part in the shuffles
+                    const int src = (int)min(pos + j, 63u);
+                    const uint32_t klo = __shfl((uint32_t)key, src, 64), khi = __shfl((uint32_t)(key >> 32), src, 64);
+                    const uint64_t kj = ((uint64_t)khi << 32) | klo;
+                    const bool m = j < len;
+                    lt += m && kj < key;
+                    eqt += m && kj == key;
+                    eqb += m && kj == key && j < idx;
+                }
+                if (live) {
+                    const uint64_t newbits = (uint64_t)db + 64;
+                    const bool final_depth = newbits >= 8ull * n;
+                    const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
+                    if (eqt > 1 && eqb == 0)
+                        dq_push(a, dq, gs, eqt, (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+                    a.sa[slot] = p;
+                    if (eqt == 1 || final_depth) {
+                        a.L[slot] = lastcol_byte(blk, n, p);
+                        if (p == 0) a.prim[b] = (eqt == 1 ? slot : gs) - boff;
+                    }
+                }
+                base = nbase;
             }
-            base = nbase;
         }
+        dq_flush<256>(a, dq);
     }
-    dq_flush<256>(a, dq);
 }
 
 // List segments (lo < len <= CAP) at any depth: rotation windows gathered from the text.
 template <uint32_t NT, uint32_t CAP>
-__global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
+__device__ __forceinline__ void finish_seg_one(const DataArgs &a, const Seg4 sg, uint32_t lo)
 {
     constexpr uint32_t IPT = FinishShape<NT, CAP>::IPT;
     __shared__ uint32_t s_rest[CAP];
     __shared__ uint32_t s_cnt[FinishShape<NT, CAP>::NDIG / 2];
     __shared__ uint32_t s_tmp[NT / 64 + 2];
     __shared__ DeferQueue<kDeferQ> dq;
-    const Seg4 sg = list[blockIdx.x];
     const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
     if (len <= lo || len > CAP) return;
     dq_init(dq);
@@ -801,6 +811,14 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
     finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
+// one segment per workgroup (exact grid from the last wait; the device count guards it)
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
+                                                   const uint32_t *__restrict__ nlist_p, uint32_t lo)
+{
+    if (blockIdx.x < *nlist_p) finish_seg_one<NT, CAP>(a, list[blockIdx.x], lo);
+}
+
 
 // List segments (lo < len <= CAP) sorted by their whole next 64 rotation bits: bitonic sort of
 // (window, position) pairs in LDS, then runs of equal windows become the next round's tie
@@ -808,7 +826,7 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
 // (SURVEY App. D Zipf: median 10, max 44 bytes at 1 MiB blocks), so advancing 64 bits per
 // round instead of 12 takes a block through in ~5 rounds instead of ~20.
 template <uint32_t NT, uint32_t CAP>
-__global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list, uint32_t lo)
+__device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg, uint32_t lo)
 {
     static_assert((CAP & (CAP - 1)) == 0, "bitonic capacity");
     constexpr uint32_t Q = CAP / 4;  // deferral queue entries (the queue overlays the key array)
@@ -816,7 +834,6 @@ __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__re
     __shared__ __align__(16) uint64_t s_key[CAP];
     __shared__ uint32_t s_pos[CAP];
     __shared__ uint32_t s_tail[CAP / 32];
-    const Seg4 sg = list[blockIdx.x];
     const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
     if (len <= lo || len > CAP) return;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
@@ -903,6 +920,13 @@ __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__re
     dq_flush<NT>(a, dq);
 }
 
+template <uint32_t NT, uint32_t CAP>
+__global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list,
+                                                    const uint32_t *__restrict__ nlist_p, uint32_t lo)
+{
+    if (blockIdx.x < *nlist_p) finish_sort_one<NT, CAP>(a, list[blockIdx.x], lo);
+}
+
 // Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
 // XCD-aware: workgroup i -> lane i % 8 -> blocks b = lane mod 8. Compact records read
 // coalesced. (A persistent variant that prefetched the next bucket into registers measured
@@ -970,13 +994,12 @@ __device__ __forceinline__ uint32_t seg_blk(uint32_t w) { return w & 0xffffu; }
 // after the shared bits (or, kRunMode, from the first difference to the smallest window). Each
 // rotation's 64-bit window is kept in kbuf (by slot) so the histogram and scatter passes read it
 // coalesced instead of gathering it from the text again.
-__global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                             unsigned long long *__restrict__ segor, unsigned long long *__restrict__ segmin,
-                                             uint64_t *__restrict__ kbuf)
+__device__ __forceinline__ void dcp_one(const DataArgs &a, const Seg4 *__restrict__ segs, const DTile t,
+                                        unsigned long long *__restrict__ segor, unsigned long long *__restrict__ segmin,
+                                        uint64_t *__restrict__ kbuf)
 {
     __shared__ uint32_t s_or[2];
     __shared__ unsigned long long s_min;
-    const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
@@ -1001,6 +1024,18 @@ __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict_
     if (threadIdx.x == 0 && (s.w & kRunMode)) atomicMin(&segmin[t.seg], s_min);
 }
 
+// grid-stride over the pass's tiles (count on the device, k_tiles)
+__global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                             const uint32_t *__restrict__ ntl_p, unsigned long long *__restrict__ segor,
+                                             unsigned long long *__restrict__ segmin, uint64_t *__restrict__ kbuf)
+{
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        dcp_one(a, segs, tiles[tb], segor, segmin, kbuf);
+        __syncthreads();
+    }
+}
+
 // depth of the pass digit: the segment depth plus its shared bits (64: no digit in the window)
 __device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint32_t seg)
 {
@@ -1022,13 +1057,12 @@ __device__ __forceinline__ uint32_t run_digit(uint64_t w, uint64_t wmin)
     return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u;
 }
 
-__global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                               const unsigned long long *__restrict__ segor,
-                                               const unsigned long long *__restrict__ segmin,
-                                               const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
+__device__ __forceinline__ void dhist_one(const DataArgs &a, const Seg4 *__restrict__ segs, const DTile t, uint32_t tb,
+                                          const unsigned long long *__restrict__ segor,
+                                          const unsigned long long *__restrict__ segmin,
+                                          const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
 {
     __shared__ uint32_t h[256];
-    const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
@@ -1047,18 +1081,32 @@ __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restric
         }
     }
     __syncthreads();
-    thist[(size_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+    thist[(size_t)tb * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                               const uint32_t *__restrict__ ntl_p,
+                                               const unsigned long long *__restrict__ segor,
+                                               const unsigned long long *__restrict__ segmin,
+                                               const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
+{
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        dhist_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, thist);
+        __syncthreads();
+    }
 }
 
 // grid = nsegs; 256 threads (digits). Offsets in place; sub-segment routing. A child left
 // with >= 3/4 of its parent and still too big for a finish pass goes on in kRunMode.
-__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint2 *__restrict__ segtiles,
-                                               const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
-                                               uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove)
+__device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restrict__ segs, uint32_t sgi,
+                                          const uint2 *__restrict__ segtiles, const unsigned long long *__restrict__ segor,
+                                          uint32_t *__restrict__ thist, uint32_t *__restrict__ stot,
+                                          uint32_t *__restrict__ nomove)
 {
     __shared__ uint32_t s_tmp[8];
-    const Seg4 s = segs[blockIdx.x];
-    const uint2 tr = segtiles[blockIdx.x];
+    const Seg4 s = segs[sgi];
+    const uint2 tr = segtiles[sgi];
     const uint32_t d = threadIdx.x;
     uint32_t run = 0;
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
@@ -1070,9 +1118,9 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
     const int nz = __syncthreads_count(tot > 0);
     const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
-    stot[(size_t)blockIdx.x * 256 + d] = tot;
+    stot[(size_t)sgi * 256 + d] = tot;
     const uint32_t b = seg_blk(s.w), n = a.boffs[b + 1] - a.boffs[b];
-    const uint32_t cp = seg_cp(segor, blockIdx.x);
+    const uint32_t cp = seg_cp(segor, sgi);
     // depth of this thread's child: kRunMode digit d shares 64 - d bits with the minimum and
     // differs in the next one (d = 0: all 64 window bits equal the minimum's)
     const uint32_t add = (s.w & kRunMode) ? (d == 0 ? 64u : 64u - d + 1u) : (cp == 64 ? 64u : cp + 8u);
@@ -1097,24 +1145,35 @@ __global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restric
         }
     };
     if (nz == 1) {
-        if (d == 0) nomove[blockIdx.x] = 1;
+        if (d == 0) nomove[sgi] = 1;
         if (tot > 0) route(s.x, s.y);
     } else {
-        if (d == 0) nomove[blockIdx.x] = 0;
+        if (d == 0) nomove[sgi] = 0;
         if (tot > 0) route(s.x + base, tot);
     }
     dq_flush<256>(a, dq);
 }
 
-__global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                                  const unsigned long long *__restrict__ segor,
-                                                  const unsigned long long *__restrict__ segmin,
-                                                  const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
-                                                  const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
-                                                  uint32_t *__restrict__ sa2)
+__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint32_t *__restrict__ nseg_p,
+                                               const uint2 *__restrict__ segtiles,
+                                               const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
+                                               uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove)
+{
+    const uint32_t nseg = *nseg_p;
+    for (uint32_t i = blockIdx.x; i < nseg; i += gridDim.x) {
+        dscan_one(a, segs, i, segtiles, segor, thist, stot, nomove);
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__restrict__ segs, const DTile t, uint32_t tb,
+                                             const unsigned long long *__restrict__ segor,
+                                             const unsigned long long *__restrict__ segmin,
+                                             const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
+                                             const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
+                                             uint32_t *__restrict__ sa2)
 {
     __shared__ uint32_t cur[256];
-    const DTile t = tiles[blockIdx.x];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
@@ -1122,7 +1181,7 @@ __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__rest
     const uint32_t cp = seg_cp(segor, t.seg);
     const bool runm = (s.w & kRunMode) != 0;
     const uint64_t wmin = runm ? segmin[t.seg] : 0ull;
-    cur[threadIdx.x] = thist[(size_t)blockIdx.x * 256 + threadIdx.x];
+    cur[threadIdx.x] = thist[(size_t)tb * 256 + threadIdx.x];
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
         const uint32_t j = t.start + e;
@@ -1134,12 +1193,31 @@ __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__rest
     }
 }
 
-__global__ __launch_bounds__(256) void k_dcopy(const DTile *__restrict__ tiles, const uint32_t *__restrict__ nomove,
-                                               uint32_t *__restrict__ sa, const uint32_t *__restrict__ sa2)
+__global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+                                                  const uint32_t *__restrict__ ntl_p,
+                                                  const unsigned long long *__restrict__ segor,
+                                                  const unsigned long long *__restrict__ segmin,
+                                                  const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
+                                                  const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
+                                                  uint32_t *__restrict__ sa2)
 {
-    const DTile t = tiles[blockIdx.x];
-    if (nomove[t.seg]) return;
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) sa[t.start + e] = sa2[t.start + e];
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        dscatter_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, nomove, thist, stot, sa2);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dcopy(const DTile *__restrict__ tiles, const uint32_t *__restrict__ ntl_p,
+                                               const uint32_t *__restrict__ nomove, uint32_t *__restrict__ sa,
+                                               const uint32_t *__restrict__ sa2)
+{
+    const uint32_t ntl = *ntl_p;
+    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+        const DTile t = tiles[tb];
+        if (nomove[t.seg]) continue;
+        for (uint32_t e = threadIdx.x; e < t.len; e += 256) sa[t.start + e] = sa2[t.start + e];
+    }
 }
 
 // -------------------------------------------------------------------- lazy rank fill
@@ -1789,20 +1867,22 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     da.prim = d_prim;
     da.bflag = bflag;
     da.cnt = d_cnt;
-    Seg4 **d_lists = (Seg4 **)c->get(WS_LISTS, kNumLists * sizeof(Seg4 *) + 64);
-    // the lists the next pass appends to: a device table uploaded in stream order (kernels
-    // queued before the upload have read the previous one)
-    auto set_lists = [&](Seg4 *tiny, Seg4 *fin, Seg4 *finb, Seg4 *bigl) {
-        Seg4 *h[kNumLists];
-        h[kListTiny] = tiny;
-        h[kListFin] = fin;
-        h[kListFinb] = finb;
-        h[kListBig] = bigl;
-        h[kListGroups] = dgroups;
-        c->h2d(d_lists, h, sizeof(h));
-        Seg4 **d = d_lists;
-        da.lists = d;
+    // list buffers of the two parities: parity 0 holds what the global pass and the dense finish
+    // defer (round 1's input); round r reads parity (r - 1) & 1 and appends to parity r & 1
+    Seg4 *const lt[2] = {fint_a, fint_b}, *const lf[2] = {fin_a, fin_b}, *const lb[2] = {finb_a, finb_b};
+    Seg4 *const lg[2] = {big, big2};
+    auto set_out = [&](uint32_t par) {
+        da.lists[kListTiny] = lt[par];
+        da.lists[kListFin] = lf[par];
+        da.lists[kListFinb] = lb[par];
+        da.lists[kListBig] = lg[par];
+        da.lists[kListGroups] = dgroups;
+        da.lcnt = d_cnt->lc[par];
     };
+    // data-phase MSD tiles (built on the device, k_tiles): the big list's slots over kDTile plus
+    // one partial tile per segment
+    const size_t bcap = N / kFinCap + 2, dtcap = N / kDTile + bcap + 2;
+    static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
 
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
@@ -1810,19 +1890,17 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     bool full_sa = c->bwt_full_sa;
     for (;;) {
         da.full_sa = full_sa ? 1u : 0u;
-        Seg4 *fint_cur = fint_a, *fint_nxt = fint_b, *fin_cur = fin_a, *fin_nxt = fin_b;
-        Seg4 *finb_cur = finb_a, *finb_nxt = finb_b;
         BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
         BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
         BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
 
         // ---- data phase
         BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-        BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, finb_cur, big,
+        BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
                    d_cnt);
+        set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
-        set_lists(fint_cur, fin_cur, finb_cur, big2);
         BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
                    da, bk, rec);
 #if defined(BMH_PROF_SCATTER) || defined(BMH_PROF_DENSE)
@@ -1841,16 +1919,14 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             fprintf(stderr, "\n");
         }
 #endif
+        // List rounds: every kernel of a round reads its list lengths from the device counters
+        // and strides over them with a fixed grid, and the MSD tiles are built on the device, so
+        // the host waits once per round (for the loop condition).
         read_counters();
-        uint32_t nfin = h_cnt->lcnt[kListFin], nfint = h_cnt->lcnt[kListTiny], nfinb = h_cnt->lcnt[kListFinb];
-        uint32_t nbig = h_cnt->big;
-        Seg4 *big_cur = big, *big_nxt = big2;
-        std::vector<Seg4> hs;
-        std::vector<DTile> ht;
-        std::vector<uint2> hst;
-        static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
         int round = 0;
-        while (nfin > 0 || nfint > 0 || nfinb > 0 || nbig > 0) {
+        for (uint32_t in = 0;; in ^= 1u) {
+            const uint32_t *ic = h_cnt->lc[in];
+            if (!(ic[kListTiny] | ic[kListFin] | ic[kListFinb] | ic[kListBig])) break;
             if (dbg_lists) {  // per-round list census (diagnostics only)
                 auto census = [&](const char *name, const Seg4 *d, uint32_t cnt) {
                     std::vector<Seg4> h(cnt);
@@ -1867,94 +1943,57 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                             (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)(cnt ? dmin : 0),
                             (unsigned long long)dmax);
                 };
-                census("tiny", fint_cur, nfint);
-                census("fin", fin_cur, nfin);
-                census("finb", finb_cur, nfinb);
-                census("big", big_cur, nbig);
-                // the round's segments must be disjoint
-                std::vector<std::pair<Seg4, int>> all;
-                const Seg4 *lp[4] = {fint_cur, fin_cur, finb_cur, big_cur};
-                const uint32_t lc[4] = {nfint, nfin, nfinb, nbig};
-                for (int li = 0; li < 4; ++li) {
-                    std::vector<Seg4> h(lc[li]);
-                    c->d2h(h.data(), lp[li], lc[li] * sizeof(Seg4));
-                    c->sync();
-                    uint32_t nff = 0;
-                    for (auto &e : h) {
-                        if (e.x == 0xffffffffu) ++nff;
-                        else all.push_back({e, li});
-                    }
-                    if (nff) fprintf(stderr, "  list %d: %u unwritten entries of %u\n", li, nff, lc[li]);
-                }
-                std::sort(all.begin(), all.end(), [](auto &x, auto &y) { return x.first.x < y.first.x; });
-                int nov = 0;
-                static std::vector<std::pair<Seg4, int>> prev;
-                for (size_t i = 1; i < all.size(); ++i)
-                    if (all[i - 1].first.x + all[i - 1].first.y > all[i].first.x && nov++ < 5) {
-                        fprintf(stderr, "  overlap: list %d [%u,+%u) depth %u / list %d [%u,+%u) depth %u\n",
-                                all[i - 1].second, all[i - 1].first.x, all[i - 1].first.y, all[i - 1].first.z,
-                                all[i].second, all[i].first.x, all[i].first.y, all[i].first.z);
-                        const uint32_t x0 = all[i - 1].first.x, x1 = x0 + all[i - 1].first.y;
-                        for (auto &e : prev)
-                            if (e.first.x < x1 && e.first.x + e.first.y > x0)
-                                fprintf(stderr, "    prev round: list %d [%u,+%u) depth %u blk %u\n", e.second, e.first.x,
-                                        e.first.y, e.first.z, e.first.w);
-                    }
-                if (nov) fprintf(stderr, "  %d overlaps\n", nov);
-                prev = all;
+                census("tiny", lt[in], ic[kListTiny]);
+                census("fin", lf[in], ic[kListFin]);
+                census("finb", lb[in], ic[kListFinb]);
+                census("big", lg[in], ic[kListBig]);
             }
             ++round;
-            BMH_HIP(hipMemsetAsync(&d_cnt->lcnt[0], 0, 16, c->stream));  // the four per-round lists
-            // every pass of a round writes the other buffer of each list
-            set_lists(fint_nxt, fin_nxt, finb_nxt, big_nxt);
-            if (dbg_lists) {  // unwritten reserved slots show as all-ones entries
-                BMH_HIP(hipMemsetAsync(fint_nxt, 0xff, seg_cap * 16, c->stream));
-                BMH_HIP(hipMemsetAsync(fin_nxt, 0xff, (N / (kTinyFin + 1) + 2) * 16, c->stream));
+            const uint32_t out = in ^ 1u;
+            const uint32_t *dc = d_cnt->lc[in];
+            BMH_HIP(hipMemsetAsync(d_cnt->lc[out], 0, 16, c->stream));
+            set_out(out);
+            // exact grids from the counts read at the last wait (one segment per workgroup: the
+            // hardware's dynamic dispatch balances their very different sizes; a fixed grid
+            // striding over the list measured 40 % slower on text); the kernels also take the
+            // device count, so a grid is never too small for what they read
+            auto g = [](uint32_t want, uint32_t) { return std::max<uint32_t>(1u, want); };
+            if (ic[kListTiny])
+                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, g(cdiv(ic[kListTiny], 256), 2048), 256, 0, da, lt[in],
+                           dc + kListTiny);
+            if (ic[kListFin]) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), g(ic[kListFin], 4096), kFinSNT, 0, da,
+                           lf[in], dc + kListFin, 1u);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), g(ic[kListFin], 2048), kFinNT, 0, da,
+                           lf[in], dc + kListFin, kFinSCap);
             }
-            if (nfint > 0)
-                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, cdiv(nfint, 256), 256, 0, da, fint_cur, nfint);
-            if (nfin > 0) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), nfin, kFinSNT, 0, da, fin_cur, 1u);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), nfin, kFinNT, 0, da, fin_cur, kFinSCap);
-            }
-            if (nfinb > 0)
-                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), nfinb, kBigNT, 0, da, finb_cur, kFinCap);
-            if (nbig > 0) {
-                hs.resize(nbig);
-                c->d2h(hs.data(), big_cur, nbig * sizeof(Seg4));
-                c->sync();
-                build_tiles<Seg4, DTile>(hs, kDTile, ht, hst, [](const Seg4 &s) { return s.x; },
-                                         [](const Seg4 &s) { return s.y; });
-                const uint32_t ntl = (uint32_t)ht.size();
-                uint8_t *d_lt = (uint8_t *)c->get(WS_LTILES, ntl * sizeof(DTile) + nbig * 8 + nbig * 4 + 64);
-                DTile *d_tiles = (DTile *)d_lt;
-                uint2 *d_segtiles = (uint2 *)(d_lt + ntl * sizeof(DTile));
-                uint32_t *d_nomove = (uint32_t *)(d_lt + ntl * sizeof(DTile) + nbig * 8);
-                c->h2d(d_tiles, ht.data(), ntl * sizeof(DTile));
-                c->h2d(d_segtiles, hst.data(), nbig * 8);
-                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, (size_t)ntl * 256 * 4);
-                uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, (size_t)nbig * 256 * 4);
-                unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, (size_t)nbig * 16 + 64);
-                unsigned long long *segmin = segor + nbig;
-                BMH_HIP(hipMemsetAsync(segor, 0, (size_t)nbig * 8, c->stream));
-                BMH_HIP(hipMemsetAsync(segmin, 0xff, (size_t)nbig * 8, c->stream));
+            if (ic[kListFinb])
+                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), g(ic[kListFinb], 1024), kBigNT, 0, da,
+                           lb[in], dc + kListFinb, kFinCap);
+            if (ic[kListBig]) {
+                uint8_t *d_dt = (uint8_t *)c->get(WS_LTILES, dtcap * sizeof(DTile) + bcap * 12 + 64);
+                DTile *d_tiles = (DTile *)d_dt;
+                uint2 *d_segtiles = (uint2 *)(d_dt + dtcap * sizeof(DTile));
+                uint32_t *d_nomove = (uint32_t *)(d_dt + dtcap * sizeof(DTile) + bcap * 8);
+                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, dtcap * 256 * 4);
+                uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, bcap * 256 * 4);
+                unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, bcap * 16 + 64);
+                unsigned long long *segmin = segor + bcap;
+                const uint32_t *nseg = dc + kListBig;
+                const uint32_t gt = 2048;  // tile kernels stride over the device's tile count
+                BMH_LAUNCH(c, "bwt_dtiles", (k_tiles<Seg4, DTile>), 1, 1024, 0, lg[in], nseg, d_tiles, d_segtiles,
+                           &d_cnt->dtiles, segor, segmin);
                 // the global-pass records are no longer read: their buffer holds the windows
-                BMH_LAUNCH(c, "bwt_dcp", k_dcp, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec, thist);
-                BMH_LAUNCH(c, "bwt_dscan", k_dscan, nbig, 256, 0, da, big_cur, d_segtiles, segor, thist, stot, d_nomove);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, ntl, 256, 0, da, big_cur, d_tiles, segor, segmin, rec, d_nomove,
-                           thist, stot, sa2);
-                BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, ntl, 256, 0, d_tiles, d_nomove, sa, sa2);
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin, rec);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin, rec,
+                           thist);
+                BMH_LAUNCH(c, "bwt_dscan", k_dscan, g(ic[kListBig], 4096), 256, 0, da, lg[in], nseg, d_segtiles, segor,
+                           thist, stot, d_nomove);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin,
+                           rec, d_nomove, thist, stot, sa2);
+                BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, gt, 256, 0, d_tiles, &d_cnt->dtiles, d_nomove, sa, sa2);
             }
             read_counters();
-            nfin = h_cnt->lcnt[kListFin];
-            nfint = h_cnt->lcnt[kListTiny];
-            nfinb = h_cnt->lcnt[kListFinb];
-            nbig = h_cnt->lcnt[kListBig];
-            std::swap(fin_cur, fin_nxt);
-            std::swap(fint_cur, fint_nxt);
-            std::swap(finb_cur, finb_nxt);
-            std::swap(big_cur, big_nxt);
         }
         if (full_sa || h_cnt->flagged == 0) break;
         full_sa = true;
@@ -1964,7 +2003,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // ---- doubling phase, only if some block still holds tied groups
     wall_data.stop();
     WallPhase wall_dbl(c, "bwt_doubling");
-    const uint32_t ngroups = h_cnt->lcnt[kListGroups];
+    const uint32_t ngroups = h_cnt->lgroups;
     if (ngroups > 0) {
         uint32_t *rkA = (uint32_t *)c->get(WS_RKA, N * 4);
         uint32_t *rkB = (uint32_t *)c->get(WS_RKB, N * 4);
