@@ -51,7 +51,7 @@ enum Slot : int {
     WS_LARGE, WS_LARGE2, WS_GROUPS, WS_PREFIX, WS_SCAN_PART, WS_TILES, WS_BLOCKS, WS_OFFS,
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
-    WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
+    WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_IN3, WS_OUT3, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
     WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_COUNT_
 };
 
@@ -94,7 +94,8 @@ struct Ctx {
     bool bwt_full_sa = false;
     // host-buffer streaming (capi.cpp): copy streams and two pinned staging slots each way
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
-    uint8_t *stage_in[2] = {nullptr, nullptr}, *stage_out[2] = {nullptr, nullptr};
+    static constexpr int kStageSlots = 3;  // host-buffer streaming: batches in flight (H2D / encode / D2H)
+    uint8_t *stage_in[kStageSlots] = {}, *stage_out[kStageSlots] = {};
     size_t stage_in_size = 0, stage_out_size = 0;
 
     void *get(Slot s, size_t bytes);

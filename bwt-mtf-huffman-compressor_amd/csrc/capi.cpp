@@ -392,7 +392,7 @@ static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes)
 }
 
 // Host-buffer encode of blocks `blist` of `in` (block size bs) on one context, pipelined over
-// batches through two staging slots (BASELINE config 5):
+// batches through Ctx::kStageSlots staging slots (BASELINE config 5):
 //   loader thread : batch k+1 pageable -> pinned (parallel memcpy), H2D on the h2d stream
 //   this thread   : encode batch k (context streams), then its records D2H on the d2h stream
 //   writer thread : records of batch k-1 pinned -> recs[] (parallel memcpy)
@@ -423,6 +423,8 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
         uint64_t cap = 0;
     };
     const uint64_t cap_batch = stream_batch_bytes();
+    // (a halving tail of batch sizes, to shorten the ramp-down after the last H2D, measured no
+    // better: every new batch layout rebuilds the encode's tables on the host)
     std::vector<B> batches;
     std::vector<size_t> first;  // block-list index of each batch's first block
     for (size_t i = 0; i < blist.size();) {
@@ -450,10 +452,17 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
     }
     ensure_staging(c, in_pinned ? 1 : max_in, pout ? 1 : max_cap);
     std::vector<uint8_t *> dst(K, nullptr);  // pinned destination of each batch's records
-    uint8_t *d_in[2] = {(uint8_t *)c->get(WS_IN, max_in), (uint8_t *)c->get(WS_IN2, max_in)};
-    uint8_t *d_out[2] = {(uint8_t *)c->get(WS_OUT, max_cap), (uint8_t *)c->get(WS_OUT2, max_cap)};
-    hipEvent_t ev_h2d[2], ev_d2h[2];
-    for (int s = 0; s < 2; ++s) {
+    // kStageSlots batches in flight: the H2D of batch k waits only for the encode of k - NS
+    constexpr int NS = Ctx::kStageSlots;
+    const int ns = (int)std::min<size_t>(NS, K);
+    const Slot ws_in[NS] = {WS_IN, WS_IN2, WS_IN3}, ws_out[NS] = {WS_OUT, WS_OUT2, WS_OUT3};
+    uint8_t *d_in[NS] = {}, *d_out[NS] = {};
+    for (int s = 0; s < ns; ++s) {
+        d_in[s] = (uint8_t *)c->get(ws_in[s], max_in);
+        d_out[s] = (uint8_t *)c->get(ws_out[s], max_cap);
+    }
+    hipEvent_t ev_h2d[NS], ev_d2h[NS];
+    for (int s = 0; s < NS; ++s) {
         BMH_HIP(hipEventCreateWithFlags(&ev_h2d[s], hipEventDisableTiming));
         BMH_HIP(hipEventCreateWithFlags(&ev_d2h[s], hipEventDisableTiming));
     }
@@ -503,9 +512,9 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
     };
     std::thread loader(guarded([&] {
         for (size_t k = 0; k < K; ++k) {
-            const int s = (int)(k & 1);
-            if (!wait_for([&] { return encoded + 2 > k; })) return;  // encode k-2 has read d_in[s]
-            if (k >= 2) BMH_HIP(hipEventSynchronize(ev_h2d[s]));     // H2D k-2 has read stage_in[s]
+            const int s = (int)(k % NS);
+            if (!wait_for([&] { return encoded + NS > k; })) return;  // encode k-NS has read d_in[s]
+            if (k >= (size_t)NS) BMH_HIP(hipEventSynchronize(ev_h2d[s]));  // H2D k-NS has read stage_in[s]
             const B &bt = batches[k];
             // consecutive blocks of the input are copied as one run
             for (size_t i = 0; i < bt.blocks.size();) {
@@ -526,7 +535,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
     }));
     std::thread writer(guarded([&] {
         for (size_t k = 0; k < K; ++k) {
-            const int s = (int)(k & 1);
+            const int s = (int)(k % NS);
             if (!wait_for([&] { return d2h_issued > k; })) return;
             BMH_HIP(hipEventSynchronize(ev_d2h[s]));
             sink(first[k], batches[k].blocks.size(), pout ? dst[k] : c->stage_out[s], ro[k].data());
@@ -535,16 +544,16 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
     }));
     guarded([&] {
         for (size_t k = 0; k < K; ++k) {
-            const int s = (int)(k & 1);
+            const int s = (int)(k % NS);
             if (!wait_for([&] { return loaded > k; })) return;
             BMH_HIP(hipEventSynchronize(ev_h2d[s]));
-            if (k >= 2) BMH_HIP(hipEventSynchronize(ev_d2h[s]));  // D2H k-2 has read d_out[s]
+            if (k >= (size_t)NS) BMH_HIP(hipEventSynchronize(ev_d2h[s]));  // D2H k-NS has read d_out[s]
             const B &bt = batches[k];
             Batch b = make_batch(bt.offs.data(), (uint32_t)bt.blocks.size());
             ro[k].resize(bt.blocks.size() + 1);
             encode_blocks(c, d_in[s], b, d_out[s], bt.cap, ro[k].data());
             bump(encoded);
-            if (!wait_for([&] { return written + 2 > k; })) return;  // the writer is done with stage_out[s]
+            if (!wait_for([&] { return written + NS > k; })) return;  // the writer is done with stage_out[s]
             const uint64_t bytes = ro[k][bt.blocks.size()];
             uint8_t *to = c->stage_out[s];
             if (pout) {
@@ -559,7 +568,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
     })();
     loader.join();
     writer.join();
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NS; ++s) {
         (void)hipEventDestroy(ev_h2d[s]);
         (void)hipEventDestroy(ev_d2h[s]);
     }
@@ -724,7 +733,7 @@ void bmh_ctx_destroy(bmh_ctx *c)
     for (int s = 0; s < WS_COUNT_; ++s)
         if (c->ws[s]) (void)hipFree(c->ws[s]);
     if (c->pinned) (void)hipHostFree(c->pinned);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < Ctx::kStageSlots; ++s) {
         if (c->stage_in[s]) (void)hipHostFree(c->stage_in[s]);
         if (c->stage_out[s]) (void)hipHostFree(c->stage_out[s]);
     }

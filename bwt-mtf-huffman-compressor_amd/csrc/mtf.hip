@@ -35,17 +35,33 @@ namespace {
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 
 // Chunk length used by the host tables (<= kMtfChunk, a multiple of 64; the kernels take any
-// such length). BMH_MTF_CHUNK overrides it for experiments: the encode runs one lane per chunk
-// for ~1 ms, so the number of chunks against the CU slots decides how full its last round is.
-static uint32_t mtf_chunk_len()
+// such length). One lane walks a chunk, about 6 one-wave workgroups fit a CU (LDS), and a step
+// takes ~0.3 us: a batch with fewer chunks than one resident round of lanes leaves the GPU idle
+// while each lane walks 4096 steps (~1.2 ms whatever the batch size). Such batches take shorter
+// chunks, down to kMtfChunkMin, so they fill about one round; batches over kMtfAdaptiveMax
+// keep kMtfChunk.
+// BMH_MTF_CHUNK overrides it for experiments.
+constexpr uint32_t kMtfChunkMin = 256;
+// only batches up to this size adapt: a layout change rebuilds the MTF tables on the host, and
+// 128-256 MiB streamed batches measured slower with shorter chunks (31 -> 46 ms per GiB)
+constexpr uint64_t kMtfAdaptiveMax = 64ull << 20;
+static uint32_t mtf_chunk_len(int device, uint64_t total)
 {
-    static const uint32_t v = [] {
+    static const uint32_t env = [] {
         const char *e = getenv("BMH_MTF_CHUNK");
-        uint32_t x = e ? (uint32_t)strtoul(e, nullptr, 10) : kMtfChunk;
-        x = x < 64 ? 64 : (x > kMtfChunk ? kMtfChunk : x);
-        return x & ~63u;
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
     }();
-    return v;
+    uint64_t x = env;
+    if (!x && total > kMtfAdaptiveMax) x = kMtfChunk;
+    if (!x) {
+        static int cus[64] = {};
+        int &cu = cus[device & 63];
+        if (!cu && hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cu = 256;
+        const uint64_t lanes = (uint64_t)std::max(cu, 1) * 6 * 64;
+        x = std::max<uint64_t>(kMtfChunkMin, (total + lanes - 1) / lanes);
+    }
+    x = x < 64 ? 64 : (x > kMtfChunk ? kMtfChunk : x);
+    return (uint32_t)((x + 63) & ~63ull);
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
 
@@ -510,7 +526,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
 {
     const uint32_t nb = bt.nblocks;
     // chunk / composition tables: rebuilt and uploaded only when the batch layout changed
-    const uint64_t sig = layout_sig(2, bt.offs, 0);
+    const uint32_t clen = mtf_chunk_len(c->device, bt.total);
+    const uint64_t sig = layout_sig(2, bt.offs, clen);
     uint32_t nch, nhh, ng, npk;
     if (c->ws_tag[WS_MTF_CHUNKS] == sig) {
         nch = c->ws_aux[WS_MTF_CHUNKS][0];
@@ -529,7 +546,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
             // unaligned prefix) so the encode kernel moves whole 64-byte sectors per lane
             for (uint64_t s = 0; s < n;) {
                 const uint64_t gpos = o + s;
-                const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + mtf_chunk_len();
+                const uint64_t lim = (gpos & 63u) ? ((gpos + 63) & ~63ull) : gpos + clen;
                 const uint64_t e = std::min<uint64_t>(o + n, lim);
                 MChunk m;
                 m.block = b;
@@ -543,12 +560,18 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                 hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
         }
         cfirst[nb] = (uint32_t)hc.size();
-        // composition runs: superchunks of <= kSuper chunks (levels 1 and 3), blocks (level 2)
+        // composition runs: superchunks of `sup` chunks (levels 1 and 3), blocks (level 2); the
+        // sequential walks are sup and chunks / sup steps long, so short chunks (more of them
+        // per block) take superchunks of ~sqrt(chunks per block), at least kSuper
+        uint32_t cpb = 1;
+        for (uint32_t b = 0; b < nb; ++b) cpb = std::max(cpb, cfirst[b + 1] - cfirst[b]);
+        uint32_t sup = kSuper;
+        while (sup * sup < cpb) sup += 8;
         std::vector<CRun> r1, r2, r3;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t g0 = (uint32_t)r1.size();
-            for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += kSuper) {
-                const uint32_t g = (uint32_t)r1.size(), e = std::min(cfirst[b + 1], x + kSuper);
+            for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += sup) {
+                const uint32_t g = (uint32_t)r1.size(), e = std::min(cfirst[b + 1], x + sup);
                 r1.push_back(CRun{x, e, kIdentity, g});
                 r3.push_back(CRun{x, e, g, g});
             }

@@ -9,7 +9,7 @@ mkdir -p $o
 i=0
 for cfg in "$@"; do
     i=$((i+1))
-    env $cfg timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --decode-steps 0 \
+    env $cfg timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 \
         > $o/$i.json 2> $o/$i.err
-    python3 -c "import json,sys; d=json.load(open('$o/$i.json')); print(f\"{sys.argv[1]:40s} {d['value']:9.1f} MB/s {d['ms_per_step']:7.3f} ms  {d['parity']}\")" "$cfg"
+    python3 -c "import json,sys; d=json.loads(open('$o/$i.json').read().strip().splitlines()[-1]); print(f\"{sys.argv[1]:40s} {d['value']:9.1f} MB/s {d['ms_per_step']:7.3f} ms  {d['parity']}\")" "$cfg"
 done
