@@ -201,10 +201,13 @@ def pcie_leg(r: dist.Rank, enc: DeviceEncoder, steps: int, warmup: int) -> dict:
         if n:
             bmh._check(lib.bmh_memcpy_d2h(ctx.h, hin.ptr, enc.d_in.ptr, n), "d2h")
         olen = [0]
+        each = []
 
         def step():
+            t0 = time.perf_counter()
             if n:
                 olen[0] = ctx.compress_into(hin.a, bs, hout.a)
+            each.append((time.perf_counter() - t0) * 1e3)
         dt = dist.timed_steps(r, step, steps, warmup, lambda: None)
         recs = enc.records()
         if len(recs) > 1:
@@ -223,6 +226,7 @@ def pcie_leg(r: dist.Rank, enc: DeviceEncoder, steps: int, warmup: int) -> dict:
                      "memory), every rank at once, max over ranks",
             "graded_roofline_frac": round(mbs / 1e3 / (r.world * HBM_PEAK_GBS), 6),
             "records_equal_device_encode": bool(ok),
+            "rank0_step_ms": [round(x, 2) for x in each[warmup:]],
             "stream_batch_bytes": int(os.environ.get("BMH_STREAM_BATCH", 256 << 20))}
 
 

@@ -1780,7 +1780,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 
     // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8); the table is
     // rebuilt and uploaded only when the batch layout changed since this context's last batch
-    const uint64_t sig = layout_sig(1, bt.offs, (uintptr_t)d_in);
+    // (the table depends on the input only through its 16-byte misalignment)
+    const uint64_t sig = layout_sig(1, bt.offs, (uintptr_t)d_in & 15u);
     uint32_t nchunks;
     uint8_t *d_tab;
     if (c->ws_tag[WS_BLOCKS] == sig) {
