@@ -61,13 +61,28 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t lc[2][4];  // data phase: entries of the tiny / fin / finb / big lists of each parity
+    uint32_t lc[2][4][8];  // data phase: entries of the tiny / fin / finb / big lists of each parity, per XCD lane
     uint32_t lgroups;   // data phase: entries of the groups list (grows over the whole phase)
     uint32_t dtiles;    // tiles of the current MSD pass (k_tiles)
     uint32_t dmin_bits, flagged;
     uint32_t coop_fill, coop_groups;  // groups too long for one wave (k_group_fill / k_groups)
     uint32_t ltiles;                  // tiles of the current large-path MSD pass (k_tiles)
+    uint32_t tstart[9];               // data-phase MSD tiles of each XCD lane (k_dtiles)
 };
+// Workgroup lanes -> list sub-lists of one launch: workgroup i runs on XCD i mod 8 (v = i & 7);
+// the 8 values of v are dealt over the non-empty sub-lists (a batch of few blocks fills few
+// lanes), v -> lane[v], the r[v]-th of rep[v] workgroup lanes serving that sub-list.
+struct LaneMap {
+    uint8_t lane[8], r[8], rep[8];
+};
+__device__ __forceinline__ void lane_of(const LaneMap &m, uint32_t i, uint32_t &x, uint32_t &j0, uint32_t &step,
+                                        uint32_t nrows)
+{
+    const uint32_t v = i & 7u;
+    x = m.lane[v];
+    j0 = (i >> 3) * m.rep[v] + m.r[v];  // this workgroup's first row of sub-list x
+    step = nrows * m.rep[v];            // rows between its iterations (striding kernels)
+}
 constexpr uint32_t kCoopGroup = 8192;  // a group this long is walked by the whole grid
 constexpr uint32_t kCoopGrid = 1024;   // workgroups of the cooperative group kernels
 
@@ -94,7 +109,8 @@ struct DataArgs {
     uint32_t *prim;
     uint32_t *bflag;   // block keeps tied groups -> needs the rank phase
     Seg4 *lists[5];      // the list each deferral class appends to (kList*)
-    uint32_t *lcnt;      // their counters (cnt->lc[parity]; groups: cnt->lgroups)
+    uint32_t *lcnt;      // their counters (cnt->lc[parity], [class][lane]; groups: cnt->lgroups)
+    const uint32_t *loff;  // [class][lane] first entry of each lane's sub-list (9 per class)
     Counters *cnt;
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
 };
@@ -144,11 +160,21 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
 // The first four are refilled every round; the groups list grows over the whole data phase.
 enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListBig = 3, kListGroups = 4, kNumLists = 5 };
 
-__device__ __forceinline__ uint32_t *list_counter(const DataArgs &a, uint32_t l)
+// The tiny / fin / finb / big lists are cut into 8 sub-lists by XCD lane (block b -> lane b & 7,
+// the dense finish's mapping): every list kernel runs workgroup i on lane i & 7, so the text
+// windows a lane's rotations gather stay in one XCD's L2. A lane's sub-list is sized from the
+// bytes of its blocks (entries are disjoint runs of >= the class's minimum length), so it never
+// overflows. Queue slots: class * 8 + lane (classes 0..3), kSlotGroups for the groups list.
+constexpr uint32_t kSlotGroups = 32, kSlots = 33;
+__device__ __forceinline__ uint32_t list_slot(uint32_t l, uint32_t w) { return l == kListGroups ? kSlotGroups : l * 8 + (w & 7u); }
+__device__ __forceinline__ uint32_t *slot_counter(const DataArgs &a, uint32_t slot)
 {
-    return l == 4u ? &a.cnt->lgroups : &a.lcnt[l];
+    return slot == kSlotGroups ? &a.cnt->lgroups : &a.lcnt[slot];
 }
-__device__ __forceinline__ Seg4 *list_base(const DataArgs &a, uint32_t l) { return a.lists[l]; }
+__device__ __forceinline__ Seg4 *slot_base(const DataArgs &a, uint32_t slot)
+{
+    return slot == kSlotGroups ? a.lists[kListGroups] : a.lists[slot >> 3] + a.loff[(slot >> 3) * 9 + (slot & 7u)];
+}
 
 // A tied run of m rotations, grouped up to bit depth nd (sg = {gs, m, nd, b}): another finish
 // pass by size class, or rank doubling once it is deep (long repeats), or final when nd
@@ -173,33 +199,34 @@ __device__ __forceinline__ uint32_t defer_list(const DataArgs &a, Seg4 &sg, uint
 template <uint32_t Q>
 struct DeferQueue {
     uint32_t n;                  // entries pushed (beyond Q they went to the lists directly)
-    uint32_t cnt[kNumLists], base[kNumLists];
+    uint32_t cnt[kSlots], base[kSlots];
     Seg4 e[Q];
-    uint32_t tag[Q];             // list << 24 | index inside the list's reservation
+    uint32_t tag[Q];             // slot << 24 | index inside the slot's reservation
 };
 
 // before the first push; a barrier must separate it from the pushes
 template <uint32_t Q>
 __device__ __forceinline__ void dq_init(DeferQueue<Q> &q)
 {
-    if (threadIdx.x < kNumLists) q.cnt[threadIdx.x] = 0;
+    if (threadIdx.x < kSlots) q.cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) q.n = 0;
 }
 
 template <uint32_t Q>
 __device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q, Seg4 sg, uint32_t l)
 {
+    const uint32_t slot = list_slot(l, sg.w);
     const uint32_t i = atomicAdd(&q.n, 1u);
     if (i < Q) {
         q.e[i] = sg;
-        q.tag[i] = (l << 24) | atomicAdd(&q.cnt[l], 1u);
+        q.tag[i] = (slot << 24) | atomicAdd(&q.cnt[slot], 1u);
     } else {
-        // lanes of one wave may overflow into different lists: one aggregated append per list,
-        // each under its own branch so that the wave's active lanes share the counter (kept
-        // rolled: the overflow is rare and every push site inlines it)
+        // lanes of one wave may overflow into different sub-lists: one aggregated append per
+        // slot, each under its own branch so that the wave's active lanes share the counter
+        // (kept rolled: the overflow is rare and every push site inlines it)
 #pragma unroll 1
-        for (uint32_t k = 0; k < kNumLists; ++k)
-            if (l == k) list_base(a, k)[wave_append(list_counter(a, k))] = sg;
+        for (uint32_t k = 0; k < kSlots; ++k)
+            if (slot == k) slot_base(a, k)[wave_append(slot_counter(a, k))] = sg;
     }
 }
 
@@ -221,11 +248,11 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
     const uint32_t qn = min(q.n, Q);
     if (qn == 0) return;  // workgroup-uniform
     const uint32_t t = threadIdx.x;
-    if (t < kNumLists && q.cnt[t]) q.base[t] = atomicAdd(list_counter(a, t), q.cnt[t]);
+    if (t < kSlots && q.cnt[t]) q.base[t] = atomicAdd(slot_counter(a, t), q.cnt[t]);
     __syncthreads();
     for (uint32_t i = t; i < qn; i += NT) {
-        const uint32_t tg = q.tag[i], l = tg >> 24;
-        list_base(a, l)[q.base[l] + (tg & 0xffffffu)] = q.e[i];
+        const uint32_t tg = q.tag[i], sl = tg >> 24;
+        slot_base(a, sl)[q.base[sl] + (tg & 0xffffffu)] = q.e[i];
     }
     __syncthreads();
 }
@@ -339,7 +366,8 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
 __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs,
                                                      const uint32_t *__restrict__ bchunks,
                                                      const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
-                                                     uint2 *__restrict__ bk, Seg4 *fin, Seg4 *big, Counters *cnt)
+                                                     uint2 *__restrict__ bk, Seg4 *fin, Seg4 *big, Counters *cnt,
+                                                     const uint32_t *__restrict__ loff)
 {
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
@@ -370,10 +398,12 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
             }
     }
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
+    const uint32_t x = b & 7u;  // the block's XCD lane sub-lists (parity 0)
     if (run > kBigCap)
-        big[wave_append(&cnt->lc[0][kListBig])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[wave_append(&cnt->lc[0][kListFinb])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        fin[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
+            make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -676,14 +706,19 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 // splits across rounds); each rotation is ranked inside its segment by the next 64 rotation
 // bits with wave shuffles. Tie groups of 2-5 rotations are the common case on text, so a wave
 // per segment would leave most lanes idle.
-__global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ list,
-                                                     const uint32_t *__restrict__ nlist_p)
+__global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ lists,
+                                                     const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
+                                                     LaneMap lm)
 {
     __shared__ DeferQueue<kTinyQ> dq;
-    const uint32_t nlist = *nlist_p;
+    // workgroup i: sub-list x of its XCD lane, entries [256 j, + 256)
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    const uint32_t nlist = cnt[x];
+    const Seg4 *__restrict__ list = lists + loff[x];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     {
-        const uint32_t g0 = blockIdx.x * 256;  // the workgroup's 256 entries (exact grid)
+        const uint32_t g0 = j * 256;
         dq_init(dq);
         __syncthreads();
         const uint32_t i0 = g0 + w * 64;
@@ -811,12 +846,15 @@ __device__ __forceinline__ void finish_seg_one(const DataArgs &a, const Seg4 sg,
     finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
-// one segment per workgroup (exact grid from the last wait; the device count guards it)
+// one segment per workgroup (grid 8 x the largest lane count from the last wait)
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__restrict__ list,
-                                                   const uint32_t *__restrict__ nlist_p, uint32_t lo)
+                                                   const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
+                                                   uint32_t lo, LaneMap lm)
 {
-    if (blockIdx.x < *nlist_p) finish_seg_one<NT, CAP>(a, list[blockIdx.x], lo);
+    uint32_t x, j, step;  // sub-list of this workgroup's XCD lane, and its entry
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    if (j < cnt[x]) finish_seg_one<NT, CAP>(a, list[loff[x] + j], lo);
 }
 
 
@@ -922,9 +960,12 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
 
 template <uint32_t NT, uint32_t CAP>
 __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list,
-                                                    const uint32_t *__restrict__ nlist_p, uint32_t lo)
+                                                    const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
+                                                    uint32_t lo, LaneMap lm)
 {
-    if (blockIdx.x < *nlist_p) finish_sort_one<NT, CAP>(a, list[blockIdx.x], lo);
+    uint32_t x, j, step;  // sub-list of this workgroup's XCD lane, and its entry
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    if (j < cnt[x]) finish_sort_one<NT, CAP>(a, list[loff[x] + j], lo);
 }
 
 // Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
@@ -1026,11 +1067,13 @@ __device__ __forceinline__ void dcp_one(const DataArgs &a, const Seg4 *__restric
 
 // grid-stride over the pass's tiles (count on the device, k_tiles)
 __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                             const uint32_t *__restrict__ ntl_p, unsigned long long *__restrict__ segor,
-                                             unsigned long long *__restrict__ segmin, uint64_t *__restrict__ kbuf)
+                                             const uint32_t *__restrict__ tstart, unsigned long long *__restrict__ segor,
+                                             unsigned long long *__restrict__ segmin, uint64_t *__restrict__ kbuf, LaneMap lm)
 {
-    const uint32_t ntl = *ntl_p;
-    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+    // workgroup i strides over the tiles of its XCD lane's sub-list
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    for (uint32_t tb = tstart[x] + j; tb < tstart[x + 1]; tb += step) {
         dcp_one(a, segs, tiles[tb], segor, segmin, kbuf);
         __syncthreads();
     }
@@ -1085,13 +1128,15 @@ __device__ __forceinline__ void dhist_one(const DataArgs &a, const Seg4 *__restr
 }
 
 __global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                               const uint32_t *__restrict__ ntl_p,
+                                               const uint32_t *__restrict__ tstart,
                                                const unsigned long long *__restrict__ segor,
                                                const unsigned long long *__restrict__ segmin,
-                                               const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
+                                               const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist, LaneMap lm)
 {
-    const uint32_t ntl = *ntl_p;
-    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+    // workgroup i strides over the tiles of its XCD lane's sub-list
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    for (uint32_t tb = tstart[x] + j; tb < tstart[x + 1]; tb += step) {
         dhist_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, thist);
         __syncthreads();
     }
@@ -1154,14 +1199,16 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
     dq_flush<256>(a, dq);
 }
 
-__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint32_t *__restrict__ nseg_p,
-                                               const uint2 *__restrict__ segtiles,
+__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint32_t *__restrict__ loff,
+                                               const uint32_t *__restrict__ cnt, const uint2 *__restrict__ segtiles,
                                                const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
-                                               uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove)
+                                               uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove, LaneMap lm)
 {
-    const uint32_t nseg = *nseg_p;
-    for (uint32_t i = blockIdx.x; i < nseg; i += gridDim.x) {
-        dscan_one(a, segs, i, segtiles, segor, thist, stot, nomove);
+    // segment ids are big-list indices; workgroup i strides over its XCD lane's sub-list
+    uint32_t x, j0, step;
+    lane_of(lm, blockIdx.x, x, j0, step, gridDim.x >> 3);
+    for (uint32_t j = j0; j < cnt[x]; j += step) {
+        dscan_one(a, segs, loff[x] + j, segtiles, segor, thist, stot, nomove);
         __syncthreads();
     }
 }
@@ -1194,26 +1241,29 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
 }
 
 __global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
-                                                  const uint32_t *__restrict__ ntl_p,
+                                                  const uint32_t *__restrict__ tstart,
                                                   const unsigned long long *__restrict__ segor,
                                                   const unsigned long long *__restrict__ segmin,
                                                   const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
                                                   const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
-                                                  uint32_t *__restrict__ sa2)
+                                                  uint32_t *__restrict__ sa2, LaneMap lm)
 {
-    const uint32_t ntl = *ntl_p;
-    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+    // workgroup i strides over the tiles of its XCD lane's sub-list
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    for (uint32_t tb = tstart[x] + j; tb < tstart[x + 1]; tb += step) {
         dscatter_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, nomove, thist, stot, sa2);
         __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(256) void k_dcopy(const DTile *__restrict__ tiles, const uint32_t *__restrict__ ntl_p,
+__global__ __launch_bounds__(256) void k_dcopy(const DTile *__restrict__ tiles, const uint32_t *__restrict__ tstart,
                                                const uint32_t *__restrict__ nomove, uint32_t *__restrict__ sa,
-                                               const uint32_t *__restrict__ sa2)
+                                               const uint32_t *__restrict__ sa2, LaneMap lm)
 {
-    const uint32_t ntl = *ntl_p;
-    for (uint32_t tb = blockIdx.x; tb < ntl; tb += gridDim.x) {
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    for (uint32_t tb = tstart[x] + j; tb < tstart[x + 1]; tb += step) {
         const DTile t = tiles[tb];
         if (nomove[t.seg]) continue;
         for (uint32_t e = threadIdx.x; e < t.len; e += 256) sa[t.start + e] = sa2[t.start + e];
@@ -1403,6 +1453,48 @@ __global__ __launch_bounds__(1024) void k_tiles(const S *__restrict__ segs, cons
         carry += total;
     }
     if (threadIdx.x == 0) *ntiles = carry;
+}
+
+// Data-phase MSD tiles: the big list's lane sub-lists in lane order (tiles of lane x from
+// cnt->tstart[x]); segment ids are big-list indices (loff[x] + j). Resets the per-segment OR /
+// minimum accumulators. One workgroup.
+__global__ __launch_bounds__(1024) void k_dtiles(const Seg4 *__restrict__ segs, const uint32_t *__restrict__ loff,
+                                                 const uint32_t *__restrict__ cnt, DTile *__restrict__ tiles,
+                                                 uint2 *__restrict__ segtiles, uint32_t *__restrict__ tstart,
+                                                 unsigned long long *__restrict__ orv, unsigned long long *__restrict__ mnv)
+{
+    __shared__ uint32_t s_tmp[17];
+    uint32_t carry = 0;
+    for (uint32_t x = 0; x < 8; ++x) {
+        if (threadIdx.x == 0) tstart[x] = carry;
+        const uint32_t nseg = cnt[x], s0 = loff[x];
+        for (uint32_t base = 0; base < nseg; base += 1024) {
+            const uint32_t j = base + threadIdx.x, i = s0 + j;
+            uint32_t st = 0, ln = 0, nt = 0;
+            if (j < nseg) {
+                st = segs[i].x;
+                ln = segs[i].y;
+                nt = (ln + kDTile - 1) / kDTile;
+            }
+            uint32_t total;
+            const uint32_t ex = carry + block_excl_sum<1024>(nt, s_tmp, &total);
+            if (j < nseg) {
+                segtiles[i] = make_uint2(ex, nt);
+                for (uint32_t k = 0; k < nt; ++k) {
+                    DTile t;
+                    t.seg = i;
+                    t.start = st + k * kDTile;
+                    t.len = min(kDTile, ln - k * kDTile);
+                    t.pad = 0;
+                    tiles[ex + k] = t;
+                }
+                orv[i] = 0;
+                mnv[i] = ~0ull;
+            }
+            carry += total;
+        }
+    }
+    if (threadIdx.x == 0) tstart[8] = carry;
 }
 
 // Doubling-phase segments of <= kTinyMax (64) rotations, packed like k_finish_tiny: each wave
@@ -1782,6 +1874,24 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // rebuilt and uploaded only when the batch layout changed since this context's last batch
     // (the table depends on the input only through its 16-byte misalignment)
     const uint64_t sig = layout_sig(1, bt.offs, (uintptr_t)d_in & 15u);
+    // deferral lists cut by XCD lane (block b -> lane b & 7): each lane's sub-list holds at most
+    // (its bytes / the class's shortest entry) + 2 entries; hloff[c * 9 + x] = its first entry
+    uint32_t hloff[4 * 9];
+    size_t ccap[4];
+    {
+        uint64_t lane_bytes[8] = {};
+        for (uint32_t b = 0; b < nb; ++b) lane_bytes[b & 7] += bt.offs[b + 1] - bt.offs[b];
+        const uint64_t cmin[4] = {2, kTinyFin + 1, kFinCap + 1, kBigCap + 1};
+        for (uint32_t cl = 0; cl < 4; ++cl) {
+            uint64_t off = 0;
+            for (uint32_t x = 0; x < 8; ++x) {
+                hloff[cl * 9 + x] = (uint32_t)off;
+                off += lane_bytes[x] / cmin[cl] + 2;
+            }
+            hloff[cl * 9 + 8] = (uint32_t)off;
+            ccap[cl] = off;
+        }
+    }
     uint32_t nchunks;
     uint8_t *d_tab;
     if (c->ws_tag[WS_BLOCKS] == sig) {
@@ -1813,7 +1923,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 if (bchunks[g.block]++ == 0) bchunk0[g.block] = (uint32_t)(k * 8 + x);
             }
         nchunks = (uint32_t)chunks.size();
-        const size_t tab_bytes = (nb + 1) * 4 + nb * 8 + nchunks * sizeof(GChunk);
+        const size_t tab_bytes = (nb + 1) * 4 + nb * 8 + nchunks * sizeof(GChunk) + sizeof(hloff);
         d_tab = (uint8_t *)c->get(WS_BLOCKS, tab_bytes + 64);
         std::vector<uint8_t> h(tab_bytes);
         size_t o = 0;
@@ -1824,6 +1934,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         memcpy(&h[o], bchunk0.data(), nb * 4);
         o += nb * 4;
         memcpy(&h[o], chunks.data(), nchunks * sizeof(GChunk));
+        o += nchunks * sizeof(GChunk);
+        memcpy(&h[o], hloff, sizeof(hloff));
         c->h2d(d_tab, h.data(), tab_bytes);
         c->ws_tag[WS_BLOCKS] = sig;
         c->ws_aux[WS_BLOCKS][0] = nchunks;
@@ -1832,6 +1944,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     const uint32_t *d_bchunks = d_boffs + (nb + 1);
     const uint32_t *d_bchunk0 = d_bchunks + nb;
     const GChunk *d_chunks = (const GChunk *)(d_bchunk0 + nb);
+    const uint32_t *d_loff = (const uint32_t *)(d_chunks + nchunks);
 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
@@ -1839,17 +1952,17 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
-    // every list entry covers >= 2 positions, so N / 2 entries bound every list
-    // finish lists by size class; every entry covers > kTinyFin / > kFinCap positions
-    Seg4 *const fint_a = (Seg4 *)c->get(WS_FINT_CUR, seg_cap * 16);
-    Seg4 *const fint_b = (Seg4 *)c->get(WS_FINT_NXT, seg_cap * 16);
-    Seg4 *const fin_a = (Seg4 *)c->get(WS_FIN_CUR, (N / (kTinyFin + 1) + 2) * 16);
-    Seg4 *const fin_b = (Seg4 *)c->get(WS_FIN_NXT, (N / (kTinyFin + 1) + 2) * 16);
-    Seg4 *const finb_a = (Seg4 *)c->get(WS_FINB_CUR, (N / (kFinCap + 1) + 2) * 16);
-    Seg4 *const finb_b = (Seg4 *)c->get(WS_FINB_NXT, (N / (kFinCap + 1) + 2) * 16);
+    // every list entry covers >= 2 positions, so N / 2 entries bound every list; the finish
+    // lists by size class and XCD lane (ccap, hloff above)
+    Seg4 *const fint_a = (Seg4 *)c->get(WS_FINT_CUR, ccap[kListTiny] * 16);
+    Seg4 *const fint_b = (Seg4 *)c->get(WS_FINT_NXT, ccap[kListTiny] * 16);
+    Seg4 *const fin_a = (Seg4 *)c->get(WS_FIN_CUR, ccap[kListFin] * 16);
+    Seg4 *const fin_b = (Seg4 *)c->get(WS_FIN_NXT, ccap[kListFin] * 16);
+    Seg4 *const finb_a = (Seg4 *)c->get(WS_FINB_CUR, ccap[kListFinb] * 16);
+    Seg4 *const finb_b = (Seg4 *)c->get(WS_FINB_NXT, ccap[kListFinb] * 16);
     Seg4 *dgroups = (Seg4 *)c->get(WS_GROUPS, seg_cap * 16);
-    Seg4 *const big = (Seg4 *)c->get(WS_LARGE, (N / kFinCap + 2) * 16);
-    Seg4 *const big2 = (Seg4 *)c->get(WS_LARGE2, (N / kFinCap + 2) * 16);
+    Seg4 *const big = (Seg4 *)c->get(WS_LARGE, ccap[kListBig] * 16);
+    Seg4 *const big2 = (Seg4 *)c->get(WS_LARGE2, ccap[kListBig] * 16);
     uint32_t *bflag = (uint32_t *)c->get(WS_OFFS, nb * 4 + 64);
     uint32_t *d_prim = (uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);
     Counters *d_cnt = (Counters *)c->get(WS_COUNTERS, sizeof(Counters) + 64);
@@ -1878,11 +1991,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         da.lists[kListFinb] = lb[par];
         da.lists[kListBig] = lg[par];
         da.lists[kListGroups] = dgroups;
-        da.lcnt = d_cnt->lc[par];
+        da.lcnt = &d_cnt->lc[par][0][0];
+        da.loff = d_loff;
     };
     // data-phase MSD tiles (built on the device, k_tiles): the big list's slots over kDTile plus
     // one partial tile per segment
-    const size_t bcap = N / kFinCap + 2, dtcap = N / kDTile + bcap + 2;
+    const size_t bcap = ccap[kListBig], dtcap = N / kDTile + bcap + 2;
     static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
 
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
@@ -1898,7 +2012,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         // ---- data phase
         BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
         BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
-                   d_cnt);
+                   d_cnt, d_loff);
         set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
@@ -1926,52 +2040,72 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         read_counters();
         int round = 0;
         for (uint32_t in = 0;; in ^= 1u) {
-            const uint32_t *ic = h_cnt->lc[in];
-            if (!(ic[kListTiny] | ic[kListFin] | ic[kListFinb] | ic[kListBig])) break;
+            // per class: entries over all lanes
+            uint32_t tot[4] = {};
+            for (uint32_t cl = 0; cl < 4; ++cl)
+                for (uint32_t x = 0; x < 8; ++x) tot[cl] += h_cnt->lc[in][cl][x];
+            if (!(tot[kListTiny] | tot[kListFin] | tot[kListFinb] | tot[kListBig])) break;
             if (dbg_lists) {  // per-round list census (diagnostics only)
-                auto census = [&](const char *name, const Seg4 *d, uint32_t cnt) {
-                    std::vector<Seg4> h(cnt);
-                    c->d2h(h.data(), d, cnt * sizeof(Seg4));
-                    c->sync();
-                    uint64_t tot = 0, mx = 0, dmin = ~0ull, dmax = 0;
-                    for (auto &e : h) {
-                        tot += e.y;
-                        mx = std::max<uint64_t>(mx, e.y);
-                        dmin = std::min<uint64_t>(dmin, e.z);
-                        dmax = std::max<uint64_t>(dmax, e.z);
+                auto census = [&](const char *name, const Seg4 *d, uint32_t cl) {
+                    uint64_t segs = 0, tsum = 0, mxl = 0, dmin = ~0ull, dmax = 0;
+                    for (uint32_t x = 0; x < 8; ++x) {
+                        const uint32_t cnt = h_cnt->lc[in][cl][x];
+                        std::vector<Seg4> h(cnt);
+                        c->d2h(h.data(), d + hloff[cl * 9 + x], cnt * sizeof(Seg4));
+                        c->sync();
+                        for (auto &e : h) {
+                            tsum += e.y;
+                            mxl = std::max<uint64_t>(mxl, e.y);
+                            dmin = std::min<uint64_t>(dmin, e.z);
+                            dmax = std::max<uint64_t>(dmax, e.z);
+                        }
+                        segs += cnt;
                     }
-                    fprintf(stderr, "round %d %-5s segs %u elems %llu max %llu depth %llu..%llu\n", round, name, cnt,
-                            (unsigned long long)tot, (unsigned long long)mx, (unsigned long long)(cnt ? dmin : 0),
-                            (unsigned long long)dmax);
+                    fprintf(stderr, "round %d %-5s segs %llu elems %llu max %llu depth %llu..%llu\n", round, name,
+                            (unsigned long long)segs, (unsigned long long)tsum, (unsigned long long)mxl,
+                            (unsigned long long)(segs ? dmin : 0), (unsigned long long)dmax);
                 };
-                census("tiny", lt[in], ic[kListTiny]);
-                census("fin", lf[in], ic[kListFin]);
-                census("finb", lb[in], ic[kListFinb]);
-                census("big", lg[in], ic[kListBig]);
+                census("tiny", lt[in], kListTiny);
+                census("fin", lf[in], kListFin);
+                census("finb", lb[in], kListFinb);
+                census("big", lg[in], kListBig);
+            }
+            // workgroup lanes dealt over the non-empty sub-lists of each class; rows[cl] = the
+            // grid's rows (grid = 8 x rows) so every entry of the fullest sub-list has a workgroup
+            LaneMap lm[4];
+            uint32_t rows[4] = {};
+            for (uint32_t cl = 0; cl < 4; ++cl) {
+                uint32_t used[8], nu = 0;
+                for (uint32_t x = 0; x < 8; ++x)
+                    if (h_cnt->lc[in][cl][x]) used[nu++] = x;
+                if (!nu) used[nu++] = 0;
+                for (uint32_t v = 0; v < 8; ++v) {
+                    const uint32_t k = v % nu;
+                    lm[cl].lane[v] = (uint8_t)used[k];
+                    lm[cl].r[v] = (uint8_t)(v / nu);
+                    lm[cl].rep[v] = (uint8_t)((8 - k + nu - 1) / nu);
+                }
+                for (uint32_t v = 0; v < 8; ++v)
+                    rows[cl] = std::max(rows[cl], cdiv(h_cnt->lc[in][cl][lm[cl].lane[v]], lm[cl].rep[v]));
             }
             ++round;
             const uint32_t out = in ^ 1u;
-            const uint32_t *dc = d_cnt->lc[in];
-            BMH_HIP(hipMemsetAsync(d_cnt->lc[out], 0, 16, c->stream));
+            BMH_HIP(hipMemsetAsync(&d_cnt->lc[out][0][0], 0, sizeof(d_cnt->lc[out]), c->stream));
             set_out(out);
-            // exact grids from the counts read at the last wait (one segment per workgroup: the
-            // hardware's dynamic dispatch balances their very different sizes; a fixed grid
-            // striding over the list measured 40 % slower on text); the kernels also take the
-            // device count, so a grid is never too small for what they read
-            auto g = [](uint32_t want, uint32_t) { return std::max<uint32_t>(1u, want); };
-            if (ic[kListTiny])
-                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, g(cdiv(ic[kListTiny], 256), 2048), 256, 0, da, lt[in],
-                           dc + kListTiny);
-            if (ic[kListFin]) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), g(ic[kListFin], 4096), kFinSNT, 0, da,
-                           lf[in], dc + kListFin, 1u);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), g(ic[kListFin], 2048), kFinNT, 0, da,
-                           lf[in], dc + kListFin, kFinSCap);
+            const uint32_t *dc = &d_cnt->lc[in][0][0];
+            if (tot[kListTiny])
+                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 256), 256, 0, da, lt[in],
+                           d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny]);
+            if (tot[kListFin]) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), 8u * rows[kListFin], kFinSNT, 0, da,
+                           lf[in], d_loff + kListFin * 9, dc + kListFin * 8, 1u, lm[kListFin]);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), 8u * rows[kListFin], kFinNT, 0, da, lf[in],
+                           d_loff + kListFin * 9, dc + kListFin * 8, kFinSCap, lm[kListFin]);
             }
-            if (ic[kListFinb])
-                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), g(ic[kListFinb], 1024), kBigNT, 0, da,
-                           lb[in], dc + kListFinb, kFinCap);
-            if (ic[kListBig]) {
+            if (tot[kListFinb])
+                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), 8u * rows[kListFinb], kBigNT, 0, da,
+                           lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
+            if (tot[kListBig]) {
                 uint8_t *d_dt = (uint8_t *)c->get(WS_LTILES, dtcap * sizeof(DTile) + bcap * 12 + 64);
                 DTile *d_tiles = (DTile *)d_dt;
                 uint2 *d_segtiles = (uint2 *)(d_dt + dtcap * sizeof(DTile));
@@ -1980,19 +2114,20 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, bcap * 256 * 4);
                 unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, bcap * 16 + 64);
                 unsigned long long *segmin = segor + bcap;
-                const uint32_t *nseg = dc + kListBig;
-                const uint32_t gt = 2048;  // tile kernels stride over the device's tile count
-                BMH_LAUNCH(c, "bwt_dtiles", (k_tiles<Seg4, DTile>), 1, 1024, 0, lg[in], nseg, d_tiles, d_segtiles,
-                           &d_cnt->dtiles, segor, segmin);
+                const uint32_t *loffb = d_loff + kListBig * 9, *cntb = dc + kListBig * 8;
+                const uint32_t gt = 2048;  // tile kernels: 256 workgroups per lane, striding over its tiles
+                BMH_LAUNCH(c, "bwt_dtiles", k_dtiles, 1, 1024, 0, lg[in], loffb, cntb, d_tiles, d_segtiles,
+                           d_cnt->tstart, segor, segmin);
                 // the global-pass records are no longer read: their buffer holds the windows
-                BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin, rec);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin, rec,
-                           thist);
-                BMH_LAUNCH(c, "bwt_dscan", k_dscan, g(ic[kListBig], 4096), 256, 0, da, lg[in], nseg, d_segtiles, segor,
-                           thist, stot, d_nomove);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, 256, 0, da, lg[in], d_tiles, &d_cnt->dtiles, segor, segmin,
-                           rec, d_nomove, thist, stot, sa2);
-                BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, gt, 256, 0, d_tiles, &d_cnt->dtiles, d_nomove, sa, sa2);
+                const LaneMap &lb_ = lm[kListBig];
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec, lb_);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec,
+                           thist, lb_);
+                BMH_LAUNCH(c, "bwt_dscan", k_dscan, 8u * std::min<uint32_t>(rows[kListBig], 512u), 256, 0, da, lg[in],
+                           loffb, cntb, d_segtiles, segor, thist, stot, d_nomove, lb_);
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin,
+                           rec, d_nomove, thist, stot, sa2, lb_);
+                BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, gt, 256, 0, d_tiles, d_cnt->tstart, d_nomove, sa, sa2, lb_);
             }
             read_counters();
         }
