@@ -40,8 +40,7 @@ constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passe
 constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
 constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
-constexpr uint32_t kFinNT = 256, kFinCap = 4096;
-constexpr uint32_t kFinSNT = 128, kFinSCap = 512;  // list segments <= 512 take a small-LDS sort
+constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register bitonic sort
 constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
@@ -858,15 +857,95 @@ __global__ __launch_bounds__(NT) void k_finish_seg(DataArgs a, const Seg4 *__res
 }
 
 
-// List segments (lo < len <= CAP) sorted by their whole next 64 rotation bits: bitonic sort of
-// (window, position) pairs in LDS, then runs of equal windows become the next round's tie
-// groups at depth db + 64. On text most rotations share several bytes with their neighbours
-// (SURVEY App. D Zipf: median 10, max 44 bytes at 1 MiB blocks), so advancing 64 bits per
-// round instead of 12 takes a block through in ~5 rounds instead of ~20.
-template <uint32_t NT, uint32_t CAP>
+// List segments (lo < len <= NT * E) sorted by their whole next 64 rotation bits: bitonic sort of
+// (window, position) pairs, then runs of equal windows become the next round's tie groups at
+// depth db + 64. On text most rotations share several bytes with their neighbours (SURVEY
+// App. D Zipf: median 10, max 44 bytes at 1 MiB blocks), so advancing 64 bits per round instead
+// of 12 takes a block through in ~5 rounds instead of ~20.
+//
+// The network is register-blocked: thread t holds the E elements of indices t * E + e, so the
+// stages of distance < E compare registers, distances < 64 E swap with the partner lane by
+// shuffles, and only distances >= 64 E (segments > 64 E with NT > 64) go through LDS. Segments
+// of <= 512 rotations take one-wave workgroups: no LDS stage and no barrier in the sort.
+
+// compare-exchange of (window, position) pairs: afterwards a <= b when up, else a >= b
+__device__ __forceinline__ void rs_cx(uint64_t &ka, uint32_t &pa, uint64_t &kb, uint32_t &pb, bool up)
+{
+    const bool gt = ka > kb || (ka == kb && pa > pb);
+    const bool sw = gt == up;
+    const uint64_t k0 = ka, k1 = kb;
+    const uint32_t p0 = pa, p1 = pb;
+    ka = sw ? k1 : k0;
+    kb = sw ? k0 : k1;
+    pa = sw ? p1 : p0;
+    pb = sw ? p0 : p1;
+}
+
+// keep the smaller (keep_min) or the larger of (k, p) and the partner's (ko, po)
+__device__ __forceinline__ void rs_keep(uint64_t &k, uint32_t &p, uint64_t ko, uint32_t po, bool keep_min)
+{
+    const bool mine_gt = k > ko || (k == ko && p > po);
+    if (mine_gt == keep_min) {
+        k = ko;
+        p = po;
+    }
+}
+
+// LDS slot of index i = u * E + e for the cross-wave stages (e rotated by u: no bank conflicts)
+template <uint32_t E>
+__device__ __forceinline__ uint32_t rs_phys(uint32_t u, uint32_t e)
+{
+    return u * E + (e ^ (u & (E - 1)));
+}
+
+// Sorts the first M (power of two) of the NT * E elements ascending (the rest are +inf).
+template <uint32_t NT, uint32_t E>
+__device__ __forceinline__ void reg_bitonic(uint64_t (&k)[E], uint32_t (&p)[E], uint32_t M, uint64_t *s_key,
+                                            uint32_t *s_pos)
+{
+    const uint32_t t = threadIdx.x;
+    for (uint32_t kk = 2; kk <= M; kk <<= 1) {
+        const bool tup = ((t * E) & kk) == 0;  // direction of this thread's elements once kk >= E
+        for (uint32_t j = kk >> 1; j >= E; j >>= 1) {
+            const uint32_t m = j / E;  // partner thread t ^ m
+            const bool keep_min = ((t & m) == 0) == tup;
+            if (m >= 64) {  // workgroup-uniform: across waves, through LDS
+                __syncthreads();
+#pragma unroll
+                for (uint32_t e = 0; e < E; ++e) {
+                    s_key[rs_phys<E>(t, e)] = k[e];
+                    s_pos[rs_phys<E>(t, e)] = p[e];
+                }
+                __syncthreads();
+#pragma unroll
+                for (uint32_t e = 0; e < E; ++e)
+                    rs_keep(k[e], p[e], s_key[rs_phys<E>(t ^ m, e)], s_pos[rs_phys<E>(t ^ m, e)], keep_min);
+            } else {
+#pragma unroll
+                for (uint32_t e = 0; e < E; ++e) {
+                    const uint32_t lo = __shfl_xor((uint32_t)k[e], (int)m, 64);
+                    const uint32_t hi = __shfl_xor((uint32_t)(k[e] >> 32), (int)m, 64);
+                    const uint32_t po = __shfl_xor(p[e], (int)m, 64);
+                    rs_keep(k[e], p[e], ((uint64_t)hi << 32) | lo, po, keep_min);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t j = E / 2; j >= 1; j >>= 1) {
+            if (j < kk) {
+#pragma unroll
+                for (uint32_t e = 0; e < E; ++e)
+                    if (!(e & j)) rs_cx(k[e], p[e], k[e + j], p[e + j], ((t * E + e) & kk) == 0);
+            }
+        }
+    }
+}
+
+template <uint32_t NT, uint32_t E>
 __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg, uint32_t lo)
 {
-    static_assert((CAP & (CAP - 1)) == 0, "bitonic capacity");
+    constexpr uint32_t CAP = NT * E;
+    static_assert((E & (E - 1)) == 0 && NT % 64 == 0, "register bitonic shape");
     constexpr uint32_t Q = CAP / 4;  // deferral queue entries (the queue overlays the key array)
     static_assert(sizeof(DeferQueue<Q>) <= CAP * 8, "deferral queue overlays the windows");
     __shared__ __align__(16) uint64_t s_key[CAP];
@@ -878,54 +957,43 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
     const uint8_t *blk = a.data + boff;
     const uint32_t t = threadIdx.x;
     const uint32_t M = len <= 2 ? 2u : 1u << (32 - __builtin_clz(len - 1));  // pow2 >= len
-    for (uint32_t i = t; i < M; i += NT) {
-        uint64_t k = ~0ull;
-        uint32_t p = 0xffffffffu;
-        if (i < len) {
-            p = a.sa[gstart + i];
-            k = rot_window(blk, n, p, db);
+    // the network sorts slots [0, M): threads t < M / E hold them (slot t * E + e); the order
+    // inside is free, so the loads are coalesced (element e * R + t of the segment)
+    const uint32_t R = M >= E ? M / E : 1u;
+    uint64_t k[E];
+    uint32_t p[E];
+#pragma unroll
+    for (uint32_t e = 0; e < E; ++e) {
+        const uint32_t i = e * R + t;
+        k[e] = ~0ull;
+        p[e] = 0xffffffffu;
+        if (t < R && i < len) {
+            p[e] = a.sa[gstart + i];
+            k[e] = rot_window(blk, n, p[e], db);
         }
-        s_key[i] = k;
-        s_pos[i] = p;
     }
     for (uint32_t i = t; i < CAP / 32; i += NT) s_tail[i] = 0;
-    __syncthreads();
-    for (uint32_t k = 2; k <= M; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t q = t; q < M / 2; q += NT) {
-                const uint32_t i0 = 2 * q - (q & (j - 1)), i1 = i0 + j;
-                const uint64_t k0 = s_key[i0], k1 = s_key[i1];
-                const uint32_t p0 = s_pos[i0], p1 = s_pos[i1];
-                const bool gt = k0 > k1 || (k0 == k1 && p0 > p1);
-                if (gt == ((i0 & k) == 0)) {
-                    s_key[i0] = k1;
-                    s_key[i1] = k0;
-                    s_pos[i0] = p1;
-                    s_pos[i1] = p0;
-                }
-            }
-            // Pairs at distance <= 64 stay inside the 128-slot tile of their q / 64, and every q
-            // of a tile belongs to one wave (q = t + r * NT), so two such stages in a row need
-            // only the wave's own ordering; a wider stage, and the last one, take the barrier.
-            const uint32_t nj = j > 1 ? j >> 1 : k;  // the next stage's distance
-            if (j <= 64 && nj <= 64 && !(k == M && j == 1)) wave_sync();
-            else __syncthreads();
-        }
+    reg_bitonic<NT, E>(k, p, M, s_key, s_pos);
+    if (M > 64 * E) __syncthreads();  // the last LDS stage's reads
+#pragma unroll
+    for (uint32_t e = 0; e < E; ++e) {
+        s_key[t * E + e] = k[e];
+        s_pos[t * E + e] = p[e];
     }
+    __syncthreads();
     // runs of equal windows: tails marked in a bitset, each head finds its tail
     for (uint32_t i = t; i < len; i += NT)
         if (i + 1 == len || s_key[i + 1] != s_key[i]) atomicOr(&s_tail[i >> 5], 1u << (i & 31u));
     __syncthreads();
     const uint64_t newbits = (uint64_t)db + 64;
     const bool final_depth = newbits >= 8ull * n;
-    constexpr uint32_t IPT = CAP / NT;
-    uint32_t hm[IPT];  // run length at a run head of >= 2 equal windows, else 0
+    uint32_t hm[E];  // run length at a run head of >= 2 equal windows, else 0
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t i = t + k * NT;
-        hm[k] = 0;
+    for (uint32_t e = 0; e < E; ++e) {
+        const uint32_t i = t + e * NT;
+        hm[e] = 0;
         if (i >= len) continue;
-        const uint32_t p = s_pos[i];
+        const uint32_t pp = s_pos[i];
         const bool head = i == 0 || s_key[i - 1] != s_key[i];
         bool single = true;
         if (!(head && ((s_tail[i >> 5] >> (i & 31u)) & 1u))) {  // part of a tie run
@@ -933,13 +1001,13 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
             if (head) {
                 uint32_t w = i >> 5, bits = s_tail[w] & (0xffffffffu << (i & 31u));
                 while (bits == 0) bits = s_tail[++w];
-                hm[k] = 32 * w + __builtin_ctz(bits) + 1 - i;
+                hm[e] = 32 * w + __builtin_ctz(bits) + 1 - i;
             }
         }
-        a.sa[gstart + i] = p;
+        a.sa[gstart + i] = pp;
         if (single || final_depth) {
-            a.L[gstart + i] = lastcol_byte(blk, n, p);
-            if (p == 0) {
+            a.L[gstart + i] = lastcol_byte(blk, n, pp);
+            if (pp == 0) {
                 uint32_t gs = i;
                 if (!single)
                     while (gs > 0 && s_key[gs - 1] == s_key[i]) --gs;
@@ -953,19 +1021,19 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
     dq_init(dq);
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k)
-        if (hm[k]) dq_push(a, dq, gstart + t + k * NT, hm[k], (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
+    for (uint32_t e = 0; e < E; ++e)
+        if (hm[e]) dq_push(a, dq, gstart + t + e * NT, hm[e], (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
     dq_flush<NT>(a, dq);
 }
 
-template <uint32_t NT, uint32_t CAP>
+template <uint32_t NT, uint32_t E>
 __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list,
                                                     const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
                                                     uint32_t lo, LaneMap lm)
 {
     uint32_t x, j, step;  // sub-list of this workgroup's XCD lane, and its entry
     lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
-    if (j < cnt[x]) finish_sort_one<NT, CAP>(a, list[loff[x] + j], lo);
+    if (j < cnt[x]) finish_sort_one<NT, E>(a, list[loff[x] + j], lo);
 }
 
 // Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
@@ -2047,7 +2115,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             if (!(tot[kListTiny] | tot[kListFin] | tot[kListFinb] | tot[kListBig])) break;
             if (dbg_lists) {  // per-round list census (diagnostics only)
                 auto census = [&](const char *name, const Seg4 *d, uint32_t cl) {
-                    uint64_t segs = 0, tsum = 0, mxl = 0, dmin = ~0ull, dmax = 0;
+                    uint64_t segs = 0, tsum = 0, mxl = 0, dmin = ~0ull, dmax = 0, lg2[33] = {};
                     for (uint32_t x = 0; x < 8; ++x) {
                         const uint32_t cnt = h_cnt->lc[in][cl][x];
                         std::vector<Seg4> h(cnt);
@@ -2055,6 +2123,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                         c->sync();
                         for (auto &e : h) {
                             tsum += e.y;
+                            lg2[e.y > 1 ? 32 - __builtin_clz(e.y - 1) : 0] += e.y;
                             mxl = std::max<uint64_t>(mxl, e.y);
                             dmin = std::min<uint64_t>(dmin, e.z);
                             dmax = std::max<uint64_t>(dmax, e.z);
@@ -2064,6 +2133,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                     fprintf(stderr, "round %d %-5s segs %llu elems %llu max %llu depth %llu..%llu\n", round, name,
                             (unsigned long long)segs, (unsigned long long)tsum, (unsigned long long)mxl,
                             (unsigned long long)(segs ? dmin : 0), (unsigned long long)dmax);
+                    if (tsum) {  // elements by segment length <= 2^k
+                        fprintf(stderr, "   ");
+                        for (int k = 0; k < 33; ++k)
+                            if (lg2[k]) fprintf(stderr, " 2^%d:%llu", k, (unsigned long long)lg2[k]);
+                        fprintf(stderr, "\n");
+                    }
                 };
                 census("tiny", lt[in], kListTiny);
                 census("fin", lf[in], kListFin);
@@ -2097,10 +2172,15 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 256), 256, 0, da, lt[in],
                            d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny]);
             if (tot[kListFin]) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinSNT, kFinSCap>), 8u * rows[kListFin], kFinSNT, 0, da,
-                           lf[in], d_loff + kListFin * 9, dc + kListFin * 8, 1u, lm[kListFin]);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<kFinNT, kFinCap>), 8u * rows[kListFin], kFinNT, 0, da, lf[in],
-                           d_loff + kListFin * 9, dc + kListFin * 8, kFinSCap, lm[kListFin]);
+                // size classes: <= 128 and <= 512 one wave each, then 2, 4 and 8 waves of 8 elements a
+                // thread (every wave of a class holds slots of its segments' sorting network)
+                const uint32_t gf = 8u * rows[kListFin];
+                const uint32_t *lof = d_loff + kListFin * 9, *cf = dc + kListFin * 8;
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 2>), gf, 64, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 8>), gf, 64, 0, da, lf[in], lof, cf, 128u, lm[kListFin]);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<128, 8>), gf, 128, 0, da, lf[in], lof, cf, 512u, lm[kListFin]);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<256, 8>), gf, 256, 0, da, lf[in], lof, cf, 1024u, lm[kListFin]);
+                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<512, 8>), gf, 512, 0, da, lf[in], lof, cf, 2048u, lm[kListFin]);
             }
             if (tot[kListFinb])
                 BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), 8u * rows[kListFinb], kBigNT, 0, da,
