@@ -41,7 +41,15 @@ constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
 constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register bitonic sort
-constexpr uint32_t kBigNT = 1024, kBigCap = 19072;
+// List segments longer than the batch's big cap take MSD passes (8 bits past their shared prefix
+// per pass); shorter ones over kFinCap a counting-sort finish (12-bit digit + 32-bit ranks).
+// Large batches (throughput-bound) use kBigCapLarge: MSD down to bitonic-sized pieces measured
+// faster than the counting-sort finish on 4097-19072 (Zipf 100 MB at 1 MiB blocks 13.5 -> 11.7
+// ms). Small batches (latency-bound: Calgary) keep the counting-sort finish up to kBigCapSmall,
+// which resolves 44 bits per round where an MSD pass takes 8 (half the rounds).
+constexpr uint32_t kBigCapLarge = 4096, kBigCapSmall = 19072, kBigNT = 1024;
+constexpr uint64_t kBigCapLargeBatch = 8ull << 20;  // batches of more bytes use kBigCapLarge
+static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kDenseCap, "list classes");
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
 constexpr uint32_t kDataMaxBits = 512;          // deeper MSD ties go to rank doubling
@@ -60,7 +68,9 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
-    uint32_t lc[2][4][8];  // data phase: entries of the tiny / fin / finb / big lists of each parity, per XCD lane
+    // data phase, per parity: entries of the tiny / fin / finb / big lists per XCD lane; row 4
+    // [0]: the bitonic size classes present in the fin list (fin_class_bit)
+    uint32_t lc[2][5][8];
     uint32_t lgroups;   // data phase: entries of the groups list (grows over the whole phase)
     uint32_t dtiles;    // tiles of the current MSD pass (k_tiles)
     uint32_t dmin_bits, flagged;
@@ -112,6 +122,7 @@ struct DataArgs {
     const uint32_t *loff;  // [class][lane] first entry of each lane's sub-list (9 per class)
     Counters *cnt;
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
+    uint32_t big_cap;  // list segments longer than this take MSD passes (kBigCapLarge / kBigCapSmall)
 };
 
 __device__ __forceinline__ uint8_t lastcol_byte(const uint8_t *blk, uint32_t n, uint32_t p)
@@ -198,6 +209,7 @@ __device__ __forceinline__ uint32_t defer_list(const DataArgs &a, Seg4 &sg, uint
 template <uint32_t Q>
 struct DeferQueue {
     uint32_t n;                  // entries pushed (beyond Q they went to the lists directly)
+    uint32_t fmask;              // fin-list size classes pushed (fin_class_bit)
     uint32_t cnt[kSlots], base[kSlots];
     Seg4 e[Q];
     uint32_t tag[Q];             // slot << 24 | index inside the slot's reservation
@@ -208,13 +220,24 @@ template <uint32_t Q>
 __device__ __forceinline__ void dq_init(DeferQueue<Q> &q)
 {
     if (threadIdx.x < kSlots) q.cnt[threadIdx.x] = 0;
-    if (threadIdx.x == 0) q.n = 0;
+    if (threadIdx.x == 0) {
+        q.n = 0;
+        q.fmask = 0;
+    }
+}
+
+// the register-bitonic launch a fin-list segment of len (65..kFinCap) takes: <= 128, 512, 1024,
+// 2048, 4096; the host launches only the classes some segment of the round needs
+__device__ __forceinline__ uint32_t fin_class_bit(uint32_t len)
+{
+    return len <= 128 ? 1u : len <= 512 ? 2u : len <= 1024 ? 4u : len <= 2048 ? 8u : 16u;
 }
 
 template <uint32_t Q>
 __device__ __forceinline__ void dq_push_list(const DataArgs &a, DeferQueue<Q> &q, Seg4 sg, uint32_t l)
 {
     const uint32_t slot = list_slot(l, sg.w);
+    if (l == kListFin) atomicOr(&q.fmask, fin_class_bit(sg.y));
     const uint32_t i = atomicAdd(&q.n, 1u);
     if (i < Q) {
         q.e[i] = sg;
@@ -248,6 +271,7 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
     if (qn == 0) return;  // workgroup-uniform
     const uint32_t t = threadIdx.x;
     if (t < kSlots && q.cnt[t]) q.base[t] = atomicAdd(slot_counter(a, t), q.cnt[t]);
+    if (t == kSlots && q.fmask) atomicOr(&a.lcnt[4 * 8], q.fmask);
     __syncthreads();
     for (uint32_t i = t; i < qn; i += NT) {
         const uint32_t tg = q.tag[i], sl = tg >> 24;
@@ -365,8 +389,8 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
 __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs,
                                                      const uint32_t *__restrict__ bchunks,
                                                      const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
-                                                     uint2 *__restrict__ bk, Seg4 *fin, Seg4 *big, Counters *cnt,
-                                                     const uint32_t *__restrict__ loff)
+                                                     uint2 *__restrict__ bk, Seg4 *finb, Seg4 *big, Counters *cnt,
+                                                     const uint32_t *__restrict__ loff, uint32_t big_cap)
 {
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
@@ -398,10 +422,12 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     }
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
     const uint32_t x = b & 7u;  // the block's XCD lane sub-lists (parity 0)
-    if (run > kBigCap)
+    // buckets <= kDenseCap are the dense finish's; longer ones take MSD passes, or the
+    // counting-sort list finish up to big_cap
+    if (run > kDenseCap && run > big_cap)
         big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
     else if (run > kDenseCap)
-        fin[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
+        finb[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
             make_uint4(boffs[b] + start, run, kG1Bits, b);
 }
 
@@ -1250,7 +1276,7 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
                 a.cnt->flagged = 1;
             }
             dq_push_list(a, dq, make_uint4(gs, len, nd, b | (final_depth ? kFinalFlag : 0u)), kListGroups);
-        } else if (len <= kBigCap) {
+        } else if (len <= a.big_cap) {
             dq_push(a, dq, gs, len, nd, b, n);
         } else {
             const bool stuck = (uint64_t)len * 4 >= (uint64_t)s.y * 3;
@@ -1935,6 +1961,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 {
     const uint32_t nb = bt.nblocks;
     const uint64_t N = bt.total;
+    const uint32_t big_cap = N > kBigCapLargeBatch ? kBigCapLarge : kBigCapSmall;
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
     WallPhase wall_data(c, "bwt_data");
 
@@ -1949,7 +1976,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     {
         uint64_t lane_bytes[8] = {};
         for (uint32_t b = 0; b < nb; ++b) lane_bytes[b & 7] += bt.offs[b + 1] - bt.offs[b];
-        const uint64_t cmin[4] = {2, kTinyFin + 1, kFinCap + 1, kBigCap + 1};
+        const uint64_t cmin[4] = {2, kTinyFin + 1, kFinCap + 1, (uint64_t)big_cap + 1};
         for (uint32_t cl = 0; cl < 4; ++cl) {
             uint64_t off = 0;
             for (uint32_t x = 0; x < 8; ++x) {
@@ -2073,6 +2100,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     bool full_sa = c->bwt_full_sa;
     for (;;) {
         da.full_sa = full_sa ? 1u : 0u;
+        da.big_cap = big_cap;
         BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
         BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
         BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
@@ -2080,7 +2108,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         // ---- data phase
         BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
         BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
-                   d_cnt, d_loff);
+                   d_cnt, d_loff, big_cap);
         set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
@@ -2171,20 +2199,35 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             if (tot[kListTiny])
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 256), 256, 0, da, lt[in],
                            d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny]);
-            if (tot[kListFin]) {  // by size: <= 512 (small LDS, many workgroups per CU), then the rest
+            if (tot[kListFin]) {
                 // size classes: <= 128 and <= 512 one wave each, then 2, 4 and 8 waves of 8 elements a
-                // thread (every wave of a class holds slots of its segments' sorting network)
+                // thread (every wave of a class holds slots of its segments' sorting network);
+                // only the classes some segment of the round needs
+                const uint32_t fm = h_cnt->lc[in][4][0];
                 const uint32_t gf = 8u * rows[kListFin];
                 const uint32_t *lof = d_loff + kListFin * 9, *cf = dc + kListFin * 8;
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 2>), gf, 64, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 8>), gf, 64, 0, da, lf[in], lof, cf, 128u, lm[kListFin]);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<128, 8>), gf, 128, 0, da, lf[in], lof, cf, 512u, lm[kListFin]);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<256, 8>), gf, 256, 0, da, lf[in], lof, cf, 1024u, lm[kListFin]);
-                BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<512, 8>), gf, 512, 0, da, lf[in], lof, cf, 2048u, lm[kListFin]);
+                if (fm & 1u)
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 2>), gf, 64, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
+                if (fm & 2u)
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 8>), gf, 64, 0, da, lf[in], lof, cf, 128u, lm[kListFin]);
+                if (fm & 4u)
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<128, 8>), gf, 128, 0, da, lf[in], lof, cf, 512u,
+                               lm[kListFin]);
+                if (fm & 8u)
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<256, 8>), gf, 256, 0, da, lf[in], lof, cf, 1024u,
+                               lm[kListFin]);
+                if (fm & 16u)
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<512, 8>), gf, 512, 0, da, lf[in], lof, cf, 2048u,
+                               lm[kListFin]);
             }
-            if (tot[kListFinb])
-                BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCap>), 8u * rows[kListFinb], kBigNT, 0, da,
-                           lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
+            if (tot[kListFinb]) {  // counting-sort finish: dense shape, or 1024 threads up to kBigCapSmall
+                if (big_cap > kDenseCap)
+                    BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCapSmall>), 8u * rows[kListFinb], kBigNT, 0,
+                               da, lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
+                else
+                    BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kDenseNT, kDenseCap>), 8u * rows[kListFinb], kDenseNT, 0,
+                               da, lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
+            }
             if (tot[kListBig]) {
                 uint8_t *d_dt = (uint8_t *)c->get(WS_LTILES, dtcap * sizeof(DTile) + bcap * 12 + 64);
                 DTile *d_tiles = (DTile *)d_dt;
