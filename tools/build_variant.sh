@@ -15,8 +15,16 @@ base=$(basename "$src")
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -I"$root/include" --offload-arch=gfx950 \
     "$@" -I"$pkg/csrc" -c "$srcpath" -o "$out/$base.o"
 objs=""
+swapped=0
 for o in "$pkg"/build/*.o; do
-    [ "$(basename "$o")" = "$base.o" ] && objs="$objs $out/$base.o" || objs="$objs $o"
+    if [ "$(basename "$o")" = "$base.o" ]; then
+        objs="$objs $out/$base.o"
+        swapped=1
+    else
+        objs="$objs $o"
+    fi
 done
+# a source whose file name is no csrc/ file would leave the in-tree object in place
+[ $swapped = 1 ] || { echo "build_variant: no csrc object $base.o (name the file like its csrc/ original)" >&2; exit 1; }
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libbmh.so" $objs
 echo "$out/libbmh.so"
