@@ -65,6 +65,17 @@ constexpr uint32_t kTinyMax = 64;     // doubling-phase segments ranked by wave 
 constexpr uint32_t kDblGrid = 1024;   // fixed grid of the doubling-phase kernels (counts read on the device)
 constexpr uint32_t kMedMax = 4096;
 constexpr uint32_t kFinalFlag = 0x80000000u;
+// Big-list segments flagged kRunMode (Seg4.w bit 30) were left holding >= 3/4 of their parent by
+// the previous MSD pass (run-dominated data: a long run of one byte, e.g. the zero runs of a fax
+// image). Their pass digit is the position of the first bit where a rotation's window differs
+// from the segment's smallest window (order-preserving: sharing more bits with the minimum
+// means smaller), so a pass advances up to 64 bits instead of 8.
+constexpr uint32_t kRunMode = 1u << 30;
+// Big-list segments flagged kRecWin (Seg4.w bit 29) are global-pass buckets whose windows the
+// global pass stored (rotation bits [10, 64): 54 known bits). Their pass digit starts at most
+// kRecWinCp bits in, inside the known bits; a segment sharing all 54 bits then has one digit,
+// stays in place and goes on at depth 64 with gathered windows.
+constexpr uint32_t kRecWin = 1u << 29, kRecWinCp = 46;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
@@ -425,7 +436,8 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     // buckets <= kDenseCap are the dense finish's; longer ones take MSD passes, or the
     // counting-sort list finish up to big_cap
     if (run > kDenseCap && run > big_cap)
-        big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] = make_uint4(boffs[b] + start, run, kG1Bits, b);
+        big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] =
+            make_uint4(boffs[b] + start, run, kG1Bits, b | kRecWin);
     else if (run > kDenseCap)
         finb[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
             make_uint4(boffs[b] + start, run, kG1Bits, b);
@@ -547,8 +559,12 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
             const uint32_t P = rec_pbits(n), R = rec_rbits(P);
             const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
             rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
-        } else if (blen > 1 || a.full_sa)
+        } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
+            // a bucket for the MSD passes: its first pass reads rotation bits [10, 64) from here
+            // (MSB-aligned, low 10 bits zero) instead of gathering them (kRecWin)
+            if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << 2) & ~0x3ffull;
+        }
         if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
             if (p == 0) a.prim[b] = slot;
@@ -1116,12 +1132,6 @@ struct DTile {
     uint32_t seg, start, len, pad;
 };
 
-// Big-list segments flagged kRunMode (Seg4.w bit 30) were left holding >= 3/4 of their parent by
-// the previous MSD pass (run-dominated data: a long run of one byte, e.g. the zero runs of a fax
-// image). Their pass digit is the position of the first bit where a rotation's window differs
-// from the segment's smallest window (order-preserving: sharing more bits with the minimum
-// means smaller), so a pass advances up to 64 bits instead of 8.
-constexpr uint32_t kRunMode = 1u << 30;
 __device__ __forceinline__ uint32_t seg_blk(uint32_t w) { return w & 0xffffu; }
 
 // Bits every rotation of an MSD segment shares below its depth (OR of window XORs against
@@ -1141,11 +1151,17 @@ __device__ __forceinline__ void dcp_one(const DataArgs &a, const Seg4 *__restric
     if (threadIdx.x < 2) s_or[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_min = ~0ull;
     __syncthreads();
-    const uint64_t w0 = rot_window(blk, n, a.sa[s.x], s.z);
+    const bool recw = (s.w & kRecWin) != 0;  // windows already in kbuf
+    const uint64_t w0 = recw ? kbuf[s.x] : rot_window(blk, n, a.sa[s.x], s.z);
     uint64_t acc = 0, mn = ~0ull;
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
-        const uint64_t w = rot_window(blk, n, a.sa[t.start + e], s.z);
-        kbuf[t.start + e] = w;
+        uint64_t w;
+        if (recw) {
+            w = kbuf[t.start + e];
+        } else {
+            w = rot_window(blk, n, a.sa[t.start + e], s.z);
+            kbuf[t.start + e] = w;
+        }
         acc |= w ^ w0;
         mn = w < mn ? w : mn;
     }
@@ -1174,10 +1190,11 @@ __global__ __launch_bounds__(256) void k_dcp(DataArgs a, const Seg4 *__restrict_
 }
 
 // depth of the pass digit: the segment depth plus its shared bits (64: no digit in the window)
-__device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint32_t seg)
+__device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint32_t seg, uint32_t w)
 {
     const unsigned long long o = segor[seg];
-    return o ? (uint32_t)__builtin_clzll(o) : 64u;
+    const uint32_t cp = o ? (uint32_t)__builtin_clzll(o) : 64u;
+    return (w & kRecWin) ? min(cp, kRecWinCp) : cp;
 }
 
 // the pass digit of slot j: from the stored window, or (digit past the window) from the text
@@ -1203,7 +1220,7 @@ __device__ __forceinline__ void dhist_one(const DataArgs &a, const Seg4 *__restr
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    const uint32_t cp = seg_cp(segor, t.seg);
+    const uint32_t cp = seg_cp(segor, t.seg, s.w);
     h[threadIdx.x] = 0;
     __syncthreads();
     if (s.w & kRunMode) {
@@ -1259,7 +1276,7 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
     stot[(size_t)sgi * 256 + d] = tot;
     const uint32_t b = seg_blk(s.w), n = a.boffs[b + 1] - a.boffs[b];
-    const uint32_t cp = seg_cp(segor, sgi);
+    const uint32_t cp = seg_cp(segor, sgi, s.w);
     // depth of this thread's child: kRunMode digit d shares 64 - d bits with the minimum and
     // differs in the next one (d = 0: all 64 window bits equal the minimum's)
     const uint32_t add = (s.w & kRunMode) ? (d == 0 ? 64u : 64u - d + 1u) : (cp == 64 ? 64u : cp + 8u);
@@ -1319,7 +1336,7 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
     if (nomove[t.seg]) return;  // one digit only: nothing moves
-    const uint32_t cp = seg_cp(segor, t.seg);
+    const uint32_t cp = seg_cp(segor, t.seg, s.w);
     const bool runm = (s.w & kRunMode) != 0;
     const uint64_t wmin = runm ? segmin[t.seg] : 0ull;
     cur[threadIdx.x] = thist[(size_t)tb * 256 + threadIdx.x];
