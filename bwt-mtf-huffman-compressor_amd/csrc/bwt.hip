@@ -940,12 +940,12 @@ __device__ __forceinline__ uint32_t rs_phys(uint32_t u, uint32_t e)
     return u * E + (e ^ (u & (E - 1)));
 }
 
-// Sorts the first M (power of two) of the NT * E elements ascending (the rest are +inf).
+// Sorts the first M (power of two) of the NT * E elements ascending (the rest are +inf); t is
+// the thread's index in the NT sorting it.
 template <uint32_t NT, uint32_t E>
 __device__ __forceinline__ void reg_bitonic(uint64_t (&k)[E], uint32_t (&p)[E], uint32_t M, uint64_t *s_key,
-                                            uint32_t *s_pos)
+                                            uint32_t *s_pos, uint32_t t)
 {
-    const uint32_t t = threadIdx.x;
     for (uint32_t kk = 2; kk <= M; kk <<= 1) {
         const bool tup = ((t * E) & kk) == 0;  // direction of this thread's elements once kk >= E
         for (uint32_t j = kk >> 1; j >= E; j >>= 1) {
@@ -983,21 +983,25 @@ __device__ __forceinline__ void reg_bitonic(uint64_t (&k)[E], uint32_t (&p)[E], 
     }
 }
 
+// One segment (lo < len <= NT * E) sorted by NT threads (t = index among them; NT = 64: one wave,
+// synchronised as a wave). Leaves the sorted windows and positions in s_key / s_pos, writes SA,
+// L (resolved slots) and the primary, and returns in hm[e] the length of the tie run headed by
+// slot t + e * NT (0: no run of >= 2 starts there) for the caller to defer.
 template <uint32_t NT, uint32_t E>
-__device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg, uint32_t lo)
+__device__ __forceinline__ void sort_seg(const DataArgs &a, const Seg4 sg, uint32_t t, uint64_t *s_key, uint32_t *s_pos,
+                                         uint32_t *s_tail, uint32_t (&hm)[E])
 {
     constexpr uint32_t CAP = NT * E;
     static_assert((E & (E - 1)) == 0 && NT % 64 == 0, "register bitonic shape");
-    constexpr uint32_t Q = CAP / 4;  // deferral queue entries (the queue overlays the key array)
-    static_assert(sizeof(DeferQueue<Q>) <= CAP * 8, "deferral queue overlays the windows");
-    __shared__ __align__(16) uint64_t s_key[CAP];
-    __shared__ uint32_t s_pos[CAP];
-    __shared__ uint32_t s_tail[CAP / 32];
+    auto sync = [] {
+        if constexpr (NT == 64)
+            wave_sync();
+        else
+            __syncthreads();
+    };
     const uint32_t gstart = sg.x, len = sg.y, db = sg.z, b = sg.w;
-    if (len <= lo || len > CAP) return;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    const uint32_t t = threadIdx.x;
     const uint32_t M = len <= 2 ? 2u : 1u << (32 - __builtin_clz(len - 1));  // pow2 >= len
     // the network sorts slots [0, M): threads t < M / E hold them (slot t * E + e); the order
     // inside is free, so the loads are coalesced (element e * R + t of the segment)
@@ -1015,21 +1019,19 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
         }
     }
     for (uint32_t i = t; i < CAP / 32; i += NT) s_tail[i] = 0;
-    reg_bitonic<NT, E>(k, p, M, s_key, s_pos);
-    if (M > 64 * E) __syncthreads();  // the last LDS stage's reads
+    reg_bitonic<NT, E>(k, p, M, s_key, s_pos, t);
+    if (M > 64 * E) sync();  // the last LDS stage's reads
 #pragma unroll
     for (uint32_t e = 0; e < E; ++e) {
         s_key[t * E + e] = k[e];
         s_pos[t * E + e] = p[e];
     }
-    __syncthreads();
+    sync();
     // runs of equal windows: tails marked in a bitset, each head finds its tail
     for (uint32_t i = t; i < len; i += NT)
         if (i + 1 == len || s_key[i + 1] != s_key[i]) atomicOr(&s_tail[i >> 5], 1u << (i & 31u));
-    __syncthreads();
-    const uint64_t newbits = (uint64_t)db + 64;
-    const bool final_depth = newbits >= 8ull * n;
-    uint32_t hm[E];  // run length at a run head of >= 2 equal windows, else 0
+    sync();
+    const bool final_depth = (uint64_t)db + 64 >= 8ull * n;
 #pragma unroll
     for (uint32_t e = 0; e < E; ++e) {
         const uint32_t i = t + e * NT;
@@ -1057,25 +1059,76 @@ __device__ __forceinline__ void finish_sort_one(const DataArgs &a, const Seg4 sg
             }
         }
     }
-    // the windows are no longer needed: their LDS holds the deferral queue
-    __syncthreads();
-    DeferQueue<Q> &dq = *reinterpret_cast<DeferQueue<Q> *>(s_key);
-    dq_init(dq);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t e = 0; e < E; ++e)
-        if (hm[e]) dq_push(a, dq, gstart + t + e * NT, hm[e], (uint32_t)min<uint64_t>(newbits, 0xffffffffull), b, n);
-    dq_flush<NT>(a, dq);
 }
 
+// the tie runs sort_seg found, deferred 64 bits deeper
+template <uint32_t NT, uint32_t E, uint32_t Q>
+__device__ __forceinline__ void sort_seg_defer(const DataArgs &a, const Seg4 sg, uint32_t t, const uint32_t (&hm)[E],
+                                               DeferQueue<Q> &dq)
+{
+    const uint32_t n = a.boffs[sg.w + 1] - a.boffs[sg.w];
+    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)sg.z + 64, 0xffffffffull);
+#pragma unroll
+    for (uint32_t e = 0; e < E; ++e)
+        if (hm[e]) dq_push(a, dq, sg.x + t + e * NT, hm[e], nd, sg.w, n);
+}
+
+// Segments of 2 .. NT * E rotations (NT >= 128), one per workgroup (grid 8 x the rows of the
+// fullest sub-list from the last wait); the deferral queue overlays the windows once sorted.
 template <uint32_t NT, uint32_t E>
 __global__ __launch_bounds__(NT) void k_finish_sort(DataArgs a, const Seg4 *__restrict__ list,
                                                     const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
                                                     uint32_t lo, LaneMap lm)
 {
+    constexpr uint32_t CAP = NT * E;
+    constexpr uint32_t Q = CAP / 4;
+    static_assert(sizeof(DeferQueue<Q>) <= CAP * 8, "deferral queue overlays the windows");
+    __shared__ __align__(16) uint64_t s_key[CAP];
+    __shared__ uint32_t s_pos[CAP];
+    __shared__ uint32_t s_tail[CAP / 32];
     uint32_t x, j, step;  // sub-list of this workgroup's XCD lane, and its entry
     lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
-    if (j < cnt[x]) finish_sort_one<NT, E>(a, list[loff[x] + j], lo);
+    if (j >= cnt[x]) return;
+    const Seg4 sg = list[loff[x] + j];
+    if (sg.y <= lo || sg.y > CAP) return;
+    uint32_t hm[E];
+    sort_seg<NT, E>(a, sg, threadIdx.x, s_key, s_pos, s_tail, hm);
+    __syncthreads();
+    DeferQueue<Q> &dq = *reinterpret_cast<DeferQueue<Q> *>(s_key);
+    dq_init(dq);
+    __syncthreads();
+    sort_seg_defer<NT, E>(a, sg, threadIdx.x, hm, dq);
+    dq_flush<NT>(a, dq);
+}
+
+// Segments of 2 .. 64 E rotations, W per workgroup: one per wave (entries W j .. W j + W - 1 of
+// the sub-list), one shared deferral queue (a workgroup per segment would flush a queue, i.e.
+// take global atomics on the same few list counters, per segment).
+constexpr uint32_t kSortWQ = 256;
+template <uint32_t E, uint32_t W>
+__global__ __launch_bounds__(64 * W) void k_finish_sortw(DataArgs a, const Seg4 *__restrict__ list,
+                                                         const uint32_t *__restrict__ loff,
+                                                         const uint32_t *__restrict__ cnt, uint32_t lo, LaneMap lm)
+{
+    constexpr uint32_t CAP = 64 * E;
+    __shared__ __align__(16) uint64_t s_key[W][CAP];
+    __shared__ uint32_t s_pos[W][CAP];
+    __shared__ uint32_t s_tail[W][CAP / 32];
+    __shared__ DeferQueue<kSortWQ> dq;
+    uint32_t x, j, step;
+    lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
+    dq_init(dq);
+    __syncthreads();
+    const uint32_t wv = threadIdx.x >> 6, l = threadIdx.x & 63u, jj = j * W + wv;
+    if (jj < cnt[x]) {  // wave-uniform
+        const Seg4 sg = list[loff[x] + jj];
+        if (sg.y > lo && sg.y <= CAP) {
+            uint32_t hm[E];
+            sort_seg<64, E>(a, sg, l, s_key[wv], s_pos[wv], s_tail[wv], hm);
+            sort_seg_defer<64, E>(a, sg, l, hm, dq);
+        }
+    }
+    dq_flush<64 * W>(a, dq);
 }
 
 // Dense finish of the global pass's buckets (db = kG1Bits), one workgroup per bucket,
@@ -2217,16 +2270,16 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 256), 256, 0, da, lt[in],
                            d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny]);
             if (tot[kListFin]) {
-                // size classes: <= 128 and <= 512 one wave each, then 2, 4 and 8 waves of 8 elements a
-                // thread (every wave of a class holds slots of its segments' sorting network);
-                // only the classes some segment of the round needs
+                // size classes: <= 128 and <= 512 one wave each (4 segments per workgroup), then 2, 4
+                // and 8 waves of 8 elements a thread (every wave of a class holds slots of its
+                // segments' sorting network); only the classes some segment of the round needs
                 const uint32_t fm = h_cnt->lc[in][4][0];
-                const uint32_t gf = 8u * rows[kListFin];
+                const uint32_t gf = 8u * rows[kListFin], gw = 8u * cdiv(rows[kListFin], 4);
                 const uint32_t *lof = d_loff + kListFin * 9, *cf = dc + kListFin * 8;
                 if (fm & 1u)
-                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 2>), gf, 64, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sortw<2, 4>), gw, 256, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
                 if (fm & 2u)
-                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<64, 8>), gf, 64, 0, da, lf[in], lof, cf, 128u, lm[kListFin]);
+                    BMH_LAUNCH(c, "bwt_finish", (k_finish_sortw<8, 4>), gw, 256, 0, da, lf[in], lof, cf, 128u, lm[kListFin]);
                 if (fm & 4u)
                     BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<128, 8>), gf, 128, 0, da, lf[in], lof, cf, 512u,
                                lm[kListFin]);
