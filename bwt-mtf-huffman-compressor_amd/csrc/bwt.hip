@@ -75,7 +75,12 @@ constexpr uint32_t kRunMode = 1u << 30;
 // global pass stored (rotation bits [10, 64): 54 known bits). Their pass digit starts at most
 // kRecWinCp bits in, inside the known bits; a segment sharing all 54 bits then has one digit,
 // stays in place and goes on at depth 64 with gathered windows.
-constexpr uint32_t kRecWin = 1u << 29, kRecWinCp = 46;
+#ifndef BMH_MSD_BITS
+#define BMH_MSD_BITS 8
+#endif
+constexpr uint32_t kMsdBits = BMH_MSD_BITS, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
+static_assert(kMsdBins >= 65 && kMsdBins <= 1024, "MSD digit (run-mode digits 0..64)");
+constexpr uint32_t kRecWin = 1u << 29, kRecWinCp = 54 - kMsdBits;
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
@@ -1254,7 +1259,8 @@ __device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint
 __device__ __forceinline__ uint32_t msd_digit(const uint64_t *kbuf, uint32_t j, uint32_t cp, const uint8_t *blk, uint32_t n,
                                               uint32_t p, uint32_t depth)
 {
-    return cp <= 56 ? (uint32_t)((kbuf[j] << cp) >> 56) : (uint32_t)(rot_window(blk, n, p, depth + cp) >> 56);
+    return cp <= 64 - kMsdBits ? (uint32_t)((kbuf[j] << cp) >> (64 - kMsdBits))
+                               : (uint32_t)(rot_window(blk, n, p, depth + cp) >> (64 - kMsdBits));
 }
 
 // kRunMode digit: 0 for the smallest window, else 64 - (bits shared with it), in 1..64
@@ -1269,7 +1275,7 @@ __device__ __forceinline__ void dhist_one(const DataArgs &a, const Seg4 *__restr
                                           const unsigned long long *__restrict__ segmin,
                                           const uint64_t *__restrict__ kbuf, uint32_t *__restrict__ thist)
 {
-    __shared__ uint32_t h[256];
+    __shared__ uint32_t h[kMsdBins];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
@@ -1278,20 +1284,20 @@ __device__ __forceinline__ void dhist_one(const DataArgs &a, const Seg4 *__restr
     __syncthreads();
     if (s.w & kRunMode) {
         const uint64_t wmin = segmin[t.seg];
-        for (uint32_t e = threadIdx.x; e < t.len; e += 256) atomicAdd(&h[run_digit(kbuf[t.start + e], wmin)], 1u);
+        for (uint32_t e = threadIdx.x; e < t.len; e += kMsdBins) atomicAdd(&h[run_digit(kbuf[t.start + e], wmin)], 1u);
     } else if (cp == 64) {
         if (threadIdx.x == 0) h[0] = t.len;
     } else {
-        for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+        for (uint32_t e = threadIdx.x; e < t.len; e += kMsdBins) {
             const uint32_t j = t.start + e;
-            atomicAdd(&h[msd_digit(kbuf, j, cp, blk, n, cp <= 56 ? 0u : a.sa[j], s.z)], 1u);
+            atomicAdd(&h[msd_digit(kbuf, j, cp, blk, n, cp <= 64 - kMsdBits ? 0u : a.sa[j], s.z)], 1u);
         }
     }
     __syncthreads();
-    thist[(size_t)tb * 256 + threadIdx.x] = h[threadIdx.x];
+    thist[(size_t)tb * kMsdBins + threadIdx.x] = h[threadIdx.x];
 }
 
-__global__ __launch_bounds__(256) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+__global__ __launch_bounds__(kMsdBins) void k_dhist(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
                                                const uint32_t *__restrict__ tstart,
                                                const unsigned long long *__restrict__ segor,
                                                const unsigned long long *__restrict__ segmin,
@@ -1313,29 +1319,29 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
                                           uint32_t *__restrict__ thist, uint32_t *__restrict__ stot,
                                           uint32_t *__restrict__ nomove)
 {
-    __shared__ uint32_t s_tmp[8];
+    __shared__ uint32_t s_tmp[kMsdBins / 64 + 1];
     const Seg4 s = segs[sgi];
     const uint2 tr = segtiles[sgi];
     const uint32_t d = threadIdx.x;
     uint32_t run = 0;
     for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) {
-        const uint32_t v = thist[(size_t)t * 256 + d];
-        thist[(size_t)t * 256 + d] = run;
+        const uint32_t v = thist[(size_t)t * kMsdBins + d];
+        thist[(size_t)t * kMsdBins + d] = run;
         run += v;
     }
     const uint32_t tot = run;
     const int nz = __syncthreads_count(tot > 0);
-    const uint32_t base = block_excl_sum<256>(tot, s_tmp, nullptr);
-    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * 256 + d] += s.x + base;
-    stot[(size_t)sgi * 256 + d] = tot;
+    const uint32_t base = block_excl_sum<kMsdBins>(tot, s_tmp, nullptr);
+    for (uint32_t t = tr.x; t < tr.x + tr.y; ++t) thist[(size_t)t * kMsdBins + d] += s.x + base;
+    stot[(size_t)sgi * kMsdBins + d] = tot;
     const uint32_t b = seg_blk(s.w), n = a.boffs[b + 1] - a.boffs[b];
     const uint32_t cp = seg_cp(segor, sgi, s.w);
     // depth of this thread's child: kRunMode digit d shares 64 - d bits with the minimum and
     // differs in the next one (d = 0: all 64 window bits equal the minimum's)
-    const uint32_t add = (s.w & kRunMode) ? (d == 0 ? 64u : 64u - d + 1u) : (cp == 64 ? 64u : cp + 8u);
+    const uint32_t add = (s.w & kRunMode) ? (d == 0 ? 64u : 64u - d + 1u) : (cp == 64 ? 64u : cp + kMsdBits);
     const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)s.z + add, 0xffffffffull);
     const bool final_depth = (uint64_t)nd >= 8ull * n;
-    __shared__ DeferQueue<256> dq;
+    __shared__ DeferQueue<kMsdBins> dq;
     dq_init(dq);
     __syncthreads();
     auto route = [&](uint32_t gs, uint32_t len) {
@@ -1360,10 +1366,10 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
         if (d == 0) nomove[sgi] = 0;
         if (tot > 0) route(s.x + base, tot);
     }
-    dq_flush<256>(a, dq);
+    dq_flush<kMsdBins>(a, dq);
 }
 
-__global__ __launch_bounds__(256) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint32_t *__restrict__ loff,
+__global__ __launch_bounds__(kMsdBins) void k_dscan(DataArgs a, const Seg4 *__restrict__ segs, const uint32_t *__restrict__ loff,
                                                const uint32_t *__restrict__ cnt, const uint2 *__restrict__ segtiles,
                                                const unsigned long long *__restrict__ segor, uint32_t *__restrict__ thist,
                                                uint32_t *__restrict__ stot, uint32_t *__restrict__ nomove, LaneMap lm)
@@ -1384,7 +1390,7 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
                                              const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
                                              uint32_t *__restrict__ sa2)
 {
-    __shared__ uint32_t cur[256];
+    __shared__ uint32_t cur[kMsdBins];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
@@ -1392,19 +1398,19 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
     const uint32_t cp = seg_cp(segor, t.seg, s.w);
     const bool runm = (s.w & kRunMode) != 0;
     const uint64_t wmin = runm ? segmin[t.seg] : 0ull;
-    cur[threadIdx.x] = thist[(size_t)tb * 256 + threadIdx.x];
+    cur[threadIdx.x] = thist[(size_t)tb * kMsdBins + threadIdx.x];
     __syncthreads();
-    for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
+    for (uint32_t e = threadIdx.x; e < t.len; e += kMsdBins) {
         const uint32_t j = t.start + e;
         const uint32_t p = a.sa[j];
         const uint32_t d = runm ? run_digit(kbuf[j], wmin) : msd_digit(kbuf, j, cp, blk, n, p, s.z);
         const uint32_t slot = atomicAdd(&cur[d], 1u);
         sa2[slot] = p;
-        if (stot[(size_t)t.seg * 256 + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
+        if (stot[(size_t)t.seg * kMsdBins + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
     }
 }
 
-__global__ __launch_bounds__(256) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
+__global__ __launch_bounds__(kMsdBins) void k_dscatter(DataArgs a, const Seg4 *__restrict__ segs, const DTile *__restrict__ tiles,
                                                   const uint32_t *__restrict__ tstart,
                                                   const unsigned long long *__restrict__ segor,
                                                   const unsigned long long *__restrict__ segmin,
@@ -2303,8 +2309,8 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 DTile *d_tiles = (DTile *)d_dt;
                 uint2 *d_segtiles = (uint2 *)(d_dt + dtcap * sizeof(DTile));
                 uint32_t *d_nomove = (uint32_t *)(d_dt + dtcap * sizeof(DTile) + bcap * 8);
-                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, dtcap * 256 * 4);
-                uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, bcap * 256 * 4);
+                uint32_t *thist = (uint32_t *)c->get(WS_LTHIST, dtcap * kMsdBins * 4);
+                uint32_t *stot = (uint32_t *)c->get(WS_LSEGS, bcap * kMsdBins * 4);
                 unsigned long long *segor = (unsigned long long *)c->get(WS_SEGOR, bcap * 16 + 64);
                 unsigned long long *segmin = segor + bcap;
                 const uint32_t *loffb = d_loff + kListBig * 9, *cntb = dc + kListBig * 8;
@@ -2314,11 +2320,11 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                 // the global-pass records are no longer read: their buffer holds the windows
                 const LaneMap &lb_ = lm[kListBig];
                 BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec, lb_);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec,
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, kMsdBins, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec,
                            thist, lb_);
-                BMH_LAUNCH(c, "bwt_dscan", k_dscan, 8u * std::min<uint32_t>(rows[kListBig], 512u), 256, 0, da, lg[in],
+                BMH_LAUNCH(c, "bwt_dscan", k_dscan, 8u * std::min<uint32_t>(rows[kListBig], 512u), kMsdBins, 0, da, lg[in],
                            loffb, cntb, d_segtiles, segor, thist, stot, d_nomove, lb_);
-                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin,
+                BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, kMsdBins, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin,
                            rec, d_nomove, thist, stot, sa2, lb_);
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, gt, 256, 0, d_tiles, d_cnt->tstart, d_nomove, sa, sa2, lb_);
             }
