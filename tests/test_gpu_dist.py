@@ -1,0 +1,44 @@
+"""GPU: bench.py's N-rank path with the real libbmh encoder — 2 ranks under
+torch.distributed.run sharing the test box's GPU (BMH_DIST_BACKEND=gloo: ranks map to
+device local_rank mod device_count; the process group carries only the barriers and the
+max-over-ranks / sum-over-ranks reductions, never block data). Each rank checks its own
+records against the reference manifest (config 4, SURVEY §8e: block b -> rank b mod N).
+
+The ranks are started as child processes of this (GPU-initialised) pytest process; nothing
+here replaces a running program."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_world2_bench_on_gpu(scaling):
+    env = dict(os.environ, BMH_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling, "--no-cpu-baseline",
+           "--decode-steps", "0", "--pcie-steps", "0", "--calgary-steps", "0"]
+    if scaling == "weak":
+        cmd += ["--bytes-per-gpu", str(256 << 20)]  # 64 blocks per rank
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.strip().splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == scaling
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    nblk = 128 if scaling == "weak" else 256  # blocks over both ranks
+    assert line["parity"] == f"{nblk}/{nblk} records byte-identical to the reference manifest", line["parity"]
