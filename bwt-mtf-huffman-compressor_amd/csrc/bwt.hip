@@ -71,16 +71,19 @@ constexpr uint32_t kFinalFlag = 0x80000000u;
 // from the segment's smallest window (order-preserving: sharing more bits with the minimum
 // means smaller), so a pass advances up to 64 bits instead of 8.
 constexpr uint32_t kRunMode = 1u << 30;
-// Big-list segments flagged kRecWin (Seg4.w bit 29) are global-pass buckets whose windows the
-// global pass stored (rotation bits [10, 64): 54 known bits). Their pass digit starts at most
-// kRecWinCp bits in, inside the known bits; a segment sharing all 54 bits then has one digit,
-// stays in place and goes on at depth 64 with gathered windows.
+// Big-list segments whose windows are already in the window buffer carry the number K of
+// known window bits in Seg4.w bits 16..22 (0: gather them): the global pass's buckets (it
+// stores rotation bits [10, 64): K = 54), and MSD children, whose parent's scatter stored the
+// window shifted past the bits that pass consumed (K = parent K - consumed). The pass digit
+// starts at most K - kMsdBits bits in, inside the known bits; a segment sharing all of them then
+// has one digit, stays in place and goes on in run mode with gathered windows.
 #ifndef BMH_MSD_BITS
 #define BMH_MSD_BITS 8
 #endif
 constexpr uint32_t kMsdBits = BMH_MSD_BITS, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
 static_assert(kMsdBins >= 65 && kMsdBins <= 1024, "MSD digit (run-mode digits 0..64)");
-constexpr uint32_t kRecWin = 1u << 29, kRecWinCp = 54 - kMsdBits;
+constexpr uint32_t kWinShift = 16, kG1WinBits = 54;
+__device__ __forceinline__ uint32_t seg_known(uint32_t w) { return (w >> kWinShift) & 127u; }
 
 struct Counters {
     uint32_t tiny, med, large, large_next, groups, next, tiles, resolved;  // doubling phase
@@ -442,7 +445,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     // counting-sort list finish up to big_cap
     if (run > kDenseCap && run > big_cap)
         big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] =
-            make_uint4(boffs[b] + start, run, kG1Bits, b | kRecWin);
+            make_uint4(boffs[b] + start, run, kG1Bits, b | (kG1WinBits << kWinShift));
     else if (run > kDenseCap)
         finb[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
             make_uint4(boffs[b] + start, run, kG1Bits, b);
@@ -567,7 +570,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
             // a bucket for the MSD passes: its first pass reads rotation bits [10, 64) from here
-            // (MSB-aligned, low 10 bits zero) instead of gathering them (kRecWin)
+            // (MSB-aligned, low 10 bits zero) instead of gathering them (kG1WinBits known)
             if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << 2) & ~0x3ffull;
         }
         if (blen == 1) {
@@ -1209,7 +1212,7 @@ __device__ __forceinline__ void dcp_one(const DataArgs &a, const Seg4 *__restric
     if (threadIdx.x < 2) s_or[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_min = ~0ull;
     __syncthreads();
-    const bool recw = (s.w & kRecWin) != 0;  // windows already in kbuf
+    const bool recw = seg_known(s.w) != 0;  // windows already in kbuf
     const uint64_t w0 = recw ? kbuf[s.x] : rot_window(blk, n, a.sa[s.x], s.z);
     uint64_t acc = 0, mn = ~0ull;
     for (uint32_t e = threadIdx.x; e < t.len; e += 256) {
@@ -1252,7 +1255,8 @@ __device__ __forceinline__ uint32_t seg_cp(const unsigned long long *segor, uint
 {
     const unsigned long long o = segor[seg];
     const uint32_t cp = o ? (uint32_t)__builtin_clzll(o) : 64u;
-    return (w & kRecWin) ? min(cp, kRecWinCp) : cp;
+    const uint32_t K = seg_known(w);
+    return K ? min(cp, K - kMsdBits) : cp;
 }
 
 // the pass digit of slot j: from the stored window, or (digit past the window) from the text
@@ -1261,6 +1265,16 @@ __device__ __forceinline__ uint32_t msd_digit(const uint64_t *kbuf, uint32_t j, 
 {
     return cp <= 64 - kMsdBits ? (uint32_t)((kbuf[j] << cp) >> (64 - kMsdBits))
                                : (uint32_t)(rot_window(blk, n, p, depth + cp) >> (64 - kMsdBits));
+}
+
+// Known window bits of a (non-run-mode) segment's children after a pass whose digit starts cp
+// bits in: the parent's (64 for gathered windows) minus the cp + kMsdBits consumed; 0 (gather)
+// when fewer than a digit's worth would remain.
+__device__ __forceinline__ uint32_t child_known(uint32_t w, uint32_t cp)
+{
+    if ((w & kRunMode) || cp == 64) return 0;
+    const uint32_t K = seg_known(w) ? seg_known(w) : 64u, used = cp + kMsdBits;
+    return K >= used + kMsdBits ? K - used : 0u;
 }
 
 // kRunMode digit: 0 for the smallest window, else 64 - (bits shared with it), in 1..64
@@ -1356,7 +1370,9 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
             dq_push(a, dq, gs, len, nd, b, n);
         } else {
             const bool stuck = (uint64_t)len * 4 >= (uint64_t)s.y * 3;
-            dq_push_list(a, dq, make_uint4(gs, len, nd, b | (stuck ? kRunMode : 0u)), kListBig);
+            // a child keeps its window in the next window buffer (written by the scatter)
+            dq_push_list(a, dq, make_uint4(gs, len, nd, b | (stuck ? kRunMode : child_known(s.w, cp) << kWinShift)),
+                         kListBig);
         }
     };
     if (nz == 1) {
@@ -1388,16 +1404,17 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
                                              const unsigned long long *__restrict__ segmin,
                                              const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
                                              const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
-                                             uint32_t *__restrict__ sa2)
+                                             uint32_t *__restrict__ sa2, uint64_t *__restrict__ kbuf_next)
 {
     __shared__ uint32_t cur[kMsdBins];
     const Seg4 s = segs[t.seg];
     const uint32_t b = seg_blk(s.w), boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    if (nomove[t.seg]) return;  // one digit only: nothing moves
+    if (nomove[t.seg]) return;  // one digit only: nothing moves (the segment goes on in run mode)
     const uint32_t cp = seg_cp(segor, t.seg, s.w);
     const bool runm = (s.w & kRunMode) != 0;
     const uint64_t wmin = runm ? segmin[t.seg] : 0ull;
+    const uint32_t kc = child_known(s.w, cp), used = cp + kMsdBits;
     cur[threadIdx.x] = thist[(size_t)tb * kMsdBins + threadIdx.x];
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < t.len; e += kMsdBins) {
@@ -1406,7 +1423,11 @@ __device__ __forceinline__ void dscatter_one(const DataArgs &a, const Seg4 *__re
         const uint32_t d = runm ? run_digit(kbuf[j], wmin) : msd_digit(kbuf, j, cp, blk, n, p, s.z);
         const uint32_t slot = atomicAdd(&cur[d], 1u);
         sa2[slot] = p;
-        if (stot[(size_t)t.seg * kMsdBins + d] == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
+        const uint32_t cn = stot[(size_t)t.seg * kMsdBins + d];  // the child's length
+        // a child that returns to the big list (not in run mode) keeps its window, past this
+        // pass's bits (dscan_one routes by the same rule)
+        if (kc && cn > a.big_cap && (uint64_t)cn * 4 < (uint64_t)s.y * 3) kbuf_next[slot] = kbuf[j] << used;
+        if (cn == 1) put_final(a, b, boff, n, blk, slot, p, slot - boff);
     }
 }
 
@@ -1416,13 +1437,13 @@ __global__ __launch_bounds__(kMsdBins) void k_dscatter(DataArgs a, const Seg4 *_
                                                   const unsigned long long *__restrict__ segmin,
                                                   const uint64_t *__restrict__ kbuf, const uint32_t *__restrict__ nomove,
                                                   const uint32_t *__restrict__ thist, const uint32_t *__restrict__ stot,
-                                                  uint32_t *__restrict__ sa2, LaneMap lm)
+                                                  uint32_t *__restrict__ sa2, uint64_t *__restrict__ kbuf_next, LaneMap lm)
 {
     // workgroup i strides over the tiles of its XCD lane's sub-list
     uint32_t x, j, step;
     lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
     for (uint32_t tb = tstart[x] + j; tb < tstart[x + 1]; tb += step) {
-        dscatter_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, nomove, thist, stot, sa2);
+        dscatter_one(a, segs, tiles[tb], tb, segor, segmin, kbuf, nomove, thist, stot, sa2, kbuf_next);
         __syncthreads();
     }
 }
@@ -2174,9 +2195,11 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
     // with every SA entry stored, and the context keeps that mode while its batches need it.
     bool full_sa = c->bwt_full_sa;
+    uint64_t *kb_cur = rec, *kb_nxt = nullptr;  // MSD window buffers (see the big-list passes)
     for (;;) {
         da.full_sa = full_sa ? 1u : 0u;
         da.big_cap = big_cap;
+        if (kb_cur != rec) std::swap(kb_cur, kb_nxt);  // the global pass writes its windows into rec
         BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
         BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
         BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
@@ -2319,14 +2342,19 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                            d_cnt->tstart, segor, segmin);
                 // the global-pass records are no longer read: their buffer holds the windows
                 const LaneMap &lb_ = lm[kListBig];
-                BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec, lb_);
-                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, kMsdBins, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, rec,
+                // window buffers: the current pass reads kb_cur (the global pass's windows, or the
+                // previous pass's scatter output) and its scatter writes the children's to kb_nxt
+                if (!kb_nxt) kb_nxt = (uint64_t *)c->get(WS_KEY8B, N * 8);
+                BMH_LAUNCH(c, "bwt_dcp", k_dcp, gt, 256, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, kb_cur,
+                           lb_);
+                BMH_LAUNCH(c, "bwt_dhist", k_dhist, gt, kMsdBins, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin, kb_cur,
                            thist, lb_);
                 BMH_LAUNCH(c, "bwt_dscan", k_dscan, 8u * std::min<uint32_t>(rows[kListBig], 512u), kMsdBins, 0, da, lg[in],
                            loffb, cntb, d_segtiles, segor, thist, stot, d_nomove, lb_);
                 BMH_LAUNCH(c, "bwt_dscatter", k_dscatter, gt, kMsdBins, 0, da, lg[in], d_tiles, d_cnt->tstart, segor, segmin,
-                           rec, d_nomove, thist, stot, sa2, lb_);
+                           kb_cur, d_nomove, thist, stot, sa2, kb_nxt, lb_);
                 BMH_LAUNCH(c, "bwt_dcopy", k_dcopy, gt, 256, 0, d_tiles, d_cnt->tstart, d_nomove, sa, sa2, lb_);
+                std::swap(kb_cur, kb_nxt);
             }
             read_counters();
         }
