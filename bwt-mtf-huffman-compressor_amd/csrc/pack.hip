@@ -79,9 +79,30 @@ __global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ 
 // chunk averages <= 15.9 bits per symbol (8 on random data); longer codes take more windows,
 // each thread re-walking its 16 symbols and keeping only the words inside the window.
 constexpr uint32_t kPackImgWords = 2048;
+// Consecutive chunks per workgroup: the code table is loaded once per block run, the next
+// chunk's symbols are in flight while this one is packed, and the image is zeroed by the
+// store pass that drains it (no zeroing pass and barrier per chunk).
+#ifndef BMH_PACK_CPW
+#define BMH_PACK_CPW 4
+#endif
+constexpr uint32_t kPackCPW = BMH_PACK_CPW;
+
+__device__ __forceinline__ uint4 pack_load_syms(const uint8_t *__restrict__ mtf, const PChunk &ch, uint32_t t)
+{
+    const uint32_t i0 = t * kPackIPT;
+    uint4 v4 = make_uint4(0, 0, 0, 0);
+    if (i0 + kPackIPT <= ch.len && ((ch.start + i0) & 15u) == 0) {
+        v4 = *(const uint4 *)(mtf + ch.start + i0);
+    } else {
+        uint32_t *vw = &v4.x;
+        for (uint32_t k = 0; k < kPackIPT; ++k)
+            if (i0 + k < ch.len) vw[k >> 2] |= (uint32_t)mtf[ch.start + i0 + k] << (8 * (k & 3));
+    }
+    return v4;
+}
 
 __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ mtf, const PChunk *__restrict__ chunks,
-                                                    const DevTable *__restrict__ tabs,
+                                                    uint32_t nch, const DevTable *__restrict__ tabs,
                                                     const uint64_t *__restrict__ cboff,
                                                     const uint64_t *__restrict__ pay_offs,
                                                     const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ out,
@@ -92,106 +113,115 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     __shared__ uint32_t s_img[kPackImgWords];
     if (status && (*status & kStatusCapacity)) return;
     const uint32_t t = threadIdx.x;
-    const PChunk ch = chunks[blockIdx.x];
-    // this thread's 16 symbols first, so their latency overlaps the code-table loads
-    const uint32_t i0 = t * kPackIPT;
-    uint4 v4 = make_uint4(0, 0, 0, 0);
-    if (i0 + kPackIPT <= ch.len && ((ch.start + i0) & 15u) == 0) {
-        v4 = *(const uint4 *)(mtf + ch.start + i0);
-    } else {
-        uint32_t *vw = &v4.x;
+    const uint32_t c0 = blockIdx.x * kPackCPW, c1 = min(c0 + kPackCPW, nch);
+    for (uint32_t w = t; w < kPackImgWords; w += 256) s_img[w] = 0;
+    uint32_t tblock = ~0u;
+    PChunk ch = chunks[c0];
+    uint4 v4 = pack_load_syms(mtf, ch, t);  // this chunk's 16 symbols of the thread
+    for (uint32_t c = c0; c < c1; ++c) {
+        // the next chunk's symbols are loaded while this one is packed
+        PChunk nx = ch;
+        uint4 nv4 = make_uint4(0, 0, 0, 0);
+        if (c + 1 < c1) {
+            nx = chunks[c + 1];
+            nv4 = pack_load_syms(mtf, nx, t);
+        }
+        if (ch.block != tblock) {  // workgroup-uniform; the previous chunk's readers are past a barrier
+            const DevTable *tb_ = &tabs[ch.block];
+            s_tab[t] = (tb_->code[t] << 8) | tb_->len[t];
+            tblock = ch.block;
+            __syncthreads();
+        }
+        const uint32_t i0 = t * kPackIPT;
+        const uint32_t nsym = i0 < ch.len ? min(kPackIPT, ch.len - i0) : 0u;
+        const uint64_t P = pay_offs[ch.block] * 8;  // the block's first payload bit
+        const uint64_t G = P + cboff[c];            // this chunk's first bit
+        const uint64_t W0 = G >> 5;
+        const uint32_t sh0 = (uint32_t)(G & 31u);
+        const uint32_t *vw = &v4.x;
+        uint32_t mybits = 0;  // a chunk holds at most 4096 * 56 bits
+#pragma unroll
         for (uint32_t k = 0; k < kPackIPT; ++k)
-            if (i0 + k < ch.len) vw[k >> 2] |= (uint32_t)mtf[ch.start + i0 + k] << (8 * (k & 3));
-    }
-    const uint32_t nsym = i0 < ch.len ? min(kPackIPT, ch.len - i0) : 0u;
-    const DevTable *tb_ = &tabs[ch.block];
-    s_tab[t] = (tb_->code[t] << 8) | tb_->len[t];
-    const uint64_t P = pay_offs[ch.block] * 8;   // the block's first payload bit
-    const uint64_t G = P + cboff[blockIdx.x];    // this chunk's first bit
-    const uint64_t W0 = G >> 5;
-    const uint32_t sh0 = (uint32_t)(G & 31u);
-    __syncthreads();
-    const uint32_t *vw = &v4.x;
-    uint32_t mybits = 0;  // a chunk holds at most 4096 * 56 bits
-#pragma unroll
-    for (uint32_t k = 0; k < kPackIPT; ++k)
-        if (k < nsym) mybits += (uint32_t)s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] & 255u;
-    uint32_t total32;
-    const uint32_t tb = block_excl_sum1<256>(mybits, s_tmp, &total32) + sh0;  // bit offset from W0 * 32
-    // the block's last chunk also owns the zero pad bits up to the payload's last byte
-    // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
-    const bool last = blockIdx.x + 1 == cfirst[ch.block + 1];
-    uint64_t own_end = G + total32;
-    if (last) {
-        const uint64_t bbits = cboff[blockIdx.x] + total32;
-        const uint64_t pb = (bbits + 7) / 8;
-        own_end = P + 8 * (pb ? pb : 1);
-    }
-    if (own_end == G) return;
-    const uint32_t nwords = (uint32_t)((own_end - W0 * 32 + 31) >> 5);
-    for (uint32_t wb = 0; wb < nwords; wb += kPackImgWords) {
-        const uint32_t nw = min(kPackImgWords, nwords - wb);
-        for (uint32_t w = t; w < nw; w += 256) s_img[w] = 0;
-        __syncthreads();
-        if (nsym && (tb >> 5) < wb + nw && ((tb + mybits + 31) >> 5) > wb) {
-            // this thread's bits [tb, tb + mybits) accumulated MSB-first in a 64-bit register,
-            // flushed a word at a time: the first word may be shared with the previous thread
-            // (LDS atomicOr), words outside the window are dropped
-            uint32_t w = tb >> 5, nacc = tb & 31u;
-            const uint32_t w_head = w;
-            const bool head_shared = nacc != 0;
-            uint64_t acc = 0;
-            auto flush = [&](uint32_t word) {
-                const uint32_t wi = w - wb;
-                if (wi < nw) {
-                    if (w == w_head && head_shared) atomicOr(&s_img[wi], word);
-                    else s_img[wi] = word;
-                }
-                ++w;
-            };
-            auto push = [&](uint32_t v, uint32_t l) {  // 1 <= l <= 32 bits, MSB-first
-                acc |= ((uint64_t)v << (64 - l)) >> nacc;
-                nacc += l;
-                if (nacc >= 32) {
-                    flush((uint32_t)(acc >> 32));
-                    acc <<= 32;
-                    nacc -= 32;
-                }
-            };
-#pragma unroll
-            for (uint32_t k = 0; k < kPackIPT; ++k) {
-                const uint64_t e = k < nsym ? s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] : 0ull;
-                const uint32_t l = (uint32_t)e & 255u;
-                const uint64_t code = e >> 8;
-                if (l > 32) {  // codes longer than 32 bits (never on 8-bit alphabets in practice)
-                    push((uint32_t)(code >> 32), l - 32);
-                    push((uint32_t)code, 32);
-                } else if (l) {
-                    push((uint32_t)code, l);
-                }
-            }
-            if (nacc) {
-                const uint32_t wi = w - wb;
-                if (wi < nw) atomicOr(&s_img[wi], (uint32_t)(acc >> 32));
-            }
+            if (k < nsym) mybits += (uint32_t)s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] & 255u;
+        uint32_t total32;
+        const uint32_t tb = block_excl_sum1<256>(mybits, s_tmp, &total32) + sh0;  // bit offset from W0 * 32
+        // the block's last chunk also owns the zero pad bits up to the payload's last byte
+        // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
+        const bool last = c + 1 == cfirst[ch.block + 1];
+        uint64_t own_end = G + total32;
+        if (last) {
+            const uint64_t bbits = cboff[c] + total32;
+            const uint64_t pb = (bbits + 7) / 8;
+            own_end = P + 8 * (pb ? pb : 1);
         }
-        __syncthreads();
-        // words wholly inside [G, own_end) are stored; the edge words are shared with the
-        // neighbouring chunks / record headers: only this chunk's bits are replaced, atomically
-        for (uint32_t w = t; w < nw; w += 256) {
-            const uint64_t ws = (W0 + wb + w) * 32;
-            const uint32_t a = G > ws ? (uint32_t)(G - ws) : 0u;
-            const uint32_t e = own_end < ws + 32 ? (uint32_t)(own_end - ws) : 32u;
-            const uint32_t v = __builtin_bswap32(s_img[w]);
-            if (a == 0 && e == 32) {
-                out[W0 + wb + w] = v;
-            } else {
-                const uint32_t m = __builtin_bswap32((0xffffffffu >> a) & (0xffffffffu << (32 - e)));
-                atomicAnd(&out[W0 + wb + w], ~m);
-                atomicOr(&out[W0 + wb + w], v & m);
+        const uint32_t nwords = own_end == G ? 0u : (uint32_t)((own_end - W0 * 32 + 31) >> 5);
+        for (uint32_t wb = 0; wb < nwords; wb += kPackImgWords) {
+            const uint32_t nw = min(kPackImgWords, nwords - wb);
+            if (nsym && (tb >> 5) < wb + nw && ((tb + mybits + 31) >> 5) > wb) {
+                // this thread's bits [tb, tb + mybits) accumulated MSB-first in a 64-bit register,
+                // flushed a word at a time: the first word may be shared with the previous thread
+                // (LDS atomicOr), words outside the window are dropped
+                uint32_t w = tb >> 5, nacc = tb & 31u;
+                const uint32_t w_head = w;
+                const bool head_shared = nacc != 0;
+                uint64_t acc = 0;
+                auto flush = [&](uint32_t word) {
+                    const uint32_t wi = w - wb;
+                    if (wi < nw) {
+                        if (w == w_head && head_shared) atomicOr(&s_img[wi], word);
+                        else s_img[wi] = word;
+                    }
+                    ++w;
+                };
+                auto push = [&](uint32_t v, uint32_t l) {  // 1 <= l <= 32 bits, MSB-first
+                    acc |= ((uint64_t)v << (64 - l)) >> nacc;
+                    nacc += l;
+                    if (nacc >= 32) {
+                        flush((uint32_t)(acc >> 32));
+                        acc <<= 32;
+                        nacc -= 32;
+                    }
+                };
+#pragma unroll
+                for (uint32_t k = 0; k < kPackIPT; ++k) {
+                    const uint64_t e = k < nsym ? s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] : 0ull;
+                    const uint32_t l = (uint32_t)e & 255u;
+                    const uint64_t code = e >> 8;
+                    if (l > 32) {  // codes longer than 32 bits (never on 8-bit alphabets in practice)
+                        push((uint32_t)(code >> 32), l - 32);
+                        push((uint32_t)code, 32);
+                    } else if (l) {
+                        push((uint32_t)code, l);
+                    }
+                }
+                if (nacc) {
+                    const uint32_t wi = w - wb;
+                    if (wi < nw) atomicOr(&s_img[wi], (uint32_t)(acc >> 32));
+                }
             }
+            __syncthreads();
+            // words wholly inside [G, own_end) are stored; the edge words are shared with the
+            // neighbouring chunks / record headers: only this chunk's bits are replaced,
+            // atomically. Each word is zeroed as it is drained (the next window starts clean).
+            for (uint32_t w = t; w < nw; w += 256) {
+                const uint64_t ws = (W0 + wb + w) * 32;
+                const uint32_t a = G > ws ? (uint32_t)(G - ws) : 0u;
+                const uint32_t e = own_end < ws + 32 ? (uint32_t)(own_end - ws) : 32u;
+                const uint32_t v = __builtin_bswap32(s_img[w]);
+                s_img[w] = 0;
+                if (a == 0 && e == 32) {
+                    out[W0 + wb + w] = v;
+                } else {
+                    const uint32_t m = __builtin_bswap32((0xffffffffu >> a) & (0xffffffffu << (32 - e)));
+                    atomicAnd(&out[W0 + wb + w], ~m);
+                    atomicOr(&out[W0 + wb + w], v & m);
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
+        if (nwords == 0) __syncthreads();  // s_tmp / s_tab reuse by the next chunk
+        ch = nx;
+        v4 = nv4;
     }
 }
 
@@ -301,7 +331,8 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
     else
         BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits);
     BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
-    BMH_LAUNCH(c, "pack_write", k_pack_write, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits, d_pay_offs, d_cfirst,
+    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(nch, kPackCPW), 256, 0, d_mtf, d_chunks, nch, d_tabs, d_cbits,
+               d_pay_offs, d_cfirst,
                (uint32_t *)d_out, d_status);
 }
 
