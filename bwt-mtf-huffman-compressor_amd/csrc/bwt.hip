@@ -692,7 +692,12 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
             // the sub-buckets on random data), the rest one by one
             uint32_t rf4[4];
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) rf4[j] = s_rest[min(s0 + j, s1 - 1)];
+            for (uint32_t j = 0; j < 4; ++j) {
+                // members 2 and 3 exist for ~40 % / ~13 % of the ranked elements: the reads of
+                // lanes without them are masked off (no bank cycles)
+                rf4[j] = 0;
+                if (j < 2 || s0 + j < s1) rf4[j] = s_rest[s0 + j];
+            }
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
                 const bool in = s0 + j < s1;
