@@ -390,7 +390,9 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
         uint32_t dg[4];
         g1_load16(blk, ch.start, ch.len, e, dg);
         const uint32_t nv = min(16u, ch.len - e);
-        const uint32_t nx = blk[(uint32_t)(((uint64_t)ch.start + e + nv) % n)];
+        // the byte after the run: at most one past the block's end (cyclic), no division
+        const uint32_t ni = ch.start + e + nv;
+        const uint32_t nx = blk[ni >= n ? ni - n : ni];
         if (nv == 16) {
 #pragma unroll
             for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dg, k, 16, nx)], 1u);
