@@ -250,8 +250,14 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     }
     std::vector<uint32_t> cut(S + 1, nb);
     cut[0] = 0;
+    // BMH_SPLIT (experiments): percent of the batch in run 0 when there are two runs
+    static const int split_pct = [] {
+        const char *e = getenv("BMH_SPLIT");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v < 100 ? v : 0;
+    }();
     for (int s = 1; s < S; ++s) {
-        const uint64_t target = bt.total * s / S;
+        const uint64_t target = (S == 2 && split_pct) ? bt.total * (uint64_t)split_pct / 100 : bt.total * s / S;
         uint32_t b = cut[s - 1] + 1;
         while (b < nb - (uint32_t)(S - s) && bt.offs[b] < target) ++b;
         cut[s] = b;
