@@ -167,6 +167,66 @@ def test_pack_dev_long_codes(ctx, oracle, nsym):
     assert bmh.record_to_mtf(rec) == s.tobytes()
 
 
+def _pack_ref(stream: np.ndarray, ln: np.ndarray, code: np.ndarray) -> bytes:
+    """encode_with_huffman (main.cpp:158-172) in numpy: code words MSB-first, zero-padded to
+    whole bytes, at least one byte."""
+    words = {}
+    for v in np.unique(stream):
+        l = int(ln[v])
+        words[int(v)] = np.array([(int(code[v]) >> (l - 1 - j)) & 1 for j in range(l)], np.uint8)
+    bits = np.concatenate([words[int(v)] for v in stream]) if stream.size else np.zeros(0, np.uint8)
+    out = np.packbits(bits).tobytes()
+    return out if out else b"\x00"
+
+
+def test_pack_dev_multiblock_windows(ctx):
+    """bmh_pack_dev over three blocks at unaligned payload offsets, each with its own table:
+    block 0 spans three 4096-symbol chunks (a pack workgroup takes 4 chunks, so its table is
+    reloaded inside the workgroup at block 1's first chunk); block 1 is made of the rarest
+    symbols of a Fibonacci table (> 16 bits per symbol: the chunk image takes several LDS
+    windows, codes over 32 bits); block 2 holds one symbol. Every payload equals the numpy
+    packing of the reference's encode_with_huffman (main.cpp:158-172)."""
+    rng = np.random.default_rng(11)
+    tabs, streams = [], []
+    for b, (nsym, n) in enumerate([(24, 9000), (40, 10000), (12, 1)]):
+        fib = _fib_stream(nsym, 100 + b)
+        d = ctx.alloc(fib.size)
+        d.upload(fib)
+        freq, first = ctx.histogram_dev(d, np.array([0, fib.size], np.uint64))
+        d.free()
+        t = bmh.huffman_build(freq[0], first[0])
+        ln = np.frombuffer(bytes(t.len), np.uint8)
+        present = np.flatnonzero(ln)
+        if b == 1:  # the ten rarest symbols (codes of 30-39 bits)
+            present = present[np.argsort(ln[present])[-10:]]
+        streams.append(rng.choice(present, n).astype(np.uint8))
+        tabs.append(t)
+    refs = [_pack_ref(s, np.frombuffer(bytes(t.len), np.uint8), np.ctypeslib.as_array(t.code))
+            for s, t in zip(streams, tabs)]
+    assert len(refs[1]) * 8 > 16 * streams[1].size
+    po = np.zeros(3, np.uint64)
+    po[0] = 3
+    po[1] = po[0] + len(refs[0]) + 1
+    po[2] = po[1] + len(refs[1]) + 5
+    total = int(po[2]) + len(refs[2]) + 8
+    allm = np.concatenate(streams)
+    offs = np.array([0, streams[0].size, streams[0].size + streams[1].size, allm.size], np.uint64)
+    d_m = ctx.alloc(allm.size)
+    d_m.upload(allm)
+    d_out = ctx.alloc(total)
+    d_out.upload(np.full(total, 0xA5, np.uint8))
+    ct = (bmh.CodeTable * 3)(*tabs)
+    bmh._check(bmh.lib().bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, bmh._u64p(po)), "pack")
+    out = d_out.download(total).tobytes()
+    d_m.free()
+    d_out.free()
+    for b in range(3):
+        assert out[int(po[b]):int(po[b]) + len(refs[b])] == refs[b], f"block {b}"
+    # bytes outside the payloads are untouched (edge words are updated under a mask)
+    assert out[:3] == b"\xa5" * 3
+    assert out[int(po[0]) + len(refs[0]):int(po[1])] == b"\xa5"
+
+
 def test_mtf_long_block_chunked(ctx, oracle):
     # > 64 K symbols per block: exercises the chunk recency / composition path
     rng = np.random.default_rng(3)
