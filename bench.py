@@ -365,9 +365,9 @@ def main() -> None:
     ap.add_argument("--calgary-steps", type=int, default=10, help="timed Calgary steps (0: skip)")
     a = ap.parse_args()
 
-    # BMH_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices round-robin);
-    # the driver's runs use the default (RCCL, one rank per GPU).
-    r = dist.init(os.environ.get("BMH_DIST_BACKEND") or None)
+    # control plane over gloo (barriers + scalar reductions only, bmh/dist.py); ranks map to
+    # devices local_rank mod device_count, so N ranks can also be rehearsed on fewer GPUs
+    r = dist.init()
     world = r.world
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")

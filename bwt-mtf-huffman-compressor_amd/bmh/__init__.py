@@ -159,30 +159,40 @@ class DevBuf:
             pass
 
 
-class HostBuf:
-    """Page-locked host memory (bmh_host_alloc) viewed as a numpy uint8 array (`.a`)."""
+class _PinnedBlock:
+    """One bmh_host_alloc block. It is the base object of every numpy view of it, so the block
+    is released only when the HostBuf and the last view (hout.a[:n], slices kept by callers)
+    are gone: a view can never read freed pinned memory."""
 
     def __init__(self, ctx: "Context", nbytes: int):
-        self.ctx, self.nbytes = ctx, int(nbytes)
         p = C.c_void_p()
-        _check(lib().bmh_host_alloc(ctx.h, max(1, self.nbytes), C.byref(p)), "host_alloc")
+        _check(lib().bmh_host_alloc(ctx.h, max(1, nbytes), C.byref(p)), "host_alloc")
         self.ptr = p
-        self.a = np.ctypeslib.as_array((C.c_uint8 * max(1, self.nbytes)).from_address(p.value))[: self.nbytes]
-
-    def free(self) -> None:
-        if self.ptr:
-            self.a = None
-            lib().bmh_host_free(self.ctx.h, self.ptr)
-            self.ptr = None
 
     def __del__(self):
         try:
-            if getattr(self, "ptr", None) and self.ctx.h:
-                self.free()
+            if self.ptr:
+                lib().bmh_host_free(None, self.ptr)  # no context needed (include/bmh.h)
+                self.ptr = None
         except Exception:
             pass
 
 
+class HostBuf:
+    """Page-locked host memory (bmh_host_alloc) viewed as a numpy uint8 array (`.a`).
+    free() drops this object's hold; the memory itself goes when no view of it is left."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        blk = _PinnedBlock(ctx, self.nbytes)
+        arr = (C.c_uint8 * max(1, self.nbytes)).from_address(blk.ptr.value)
+        arr._owner = blk  # numpy views keep arr alive, arr keeps the block
+        self.ptr = blk.ptr
+        self.a = np.frombuffer(arr, dtype=np.uint8)[: self.nbytes]
+
+    def free(self) -> None:
+        self.a = None
+        self.ptr = None
 class Context:
     """One GPU (bmh_ctx). Not thread-safe; use one per device/thread."""
 

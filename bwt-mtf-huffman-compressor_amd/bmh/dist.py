@@ -1,13 +1,17 @@
 """Multi-GPU driver helpers: one process per GPU, blocks dealt round-robin, no data-path
-collective (blocks are independent — SURVEY.md §8e). torch.distributed is used only for the
-barrier around the timed region and the max-over-ranks of its duration (RCCL on GPUs, gloo
-on CPU for tests)."""
+collective (blocks are independent — SURVEY.md §8e). torch.distributed carries only the
+control plane: the barriers around the timed region and scalar max / sum reductions of its
+duration and byte counts. Those are a few host scalars per run, so the process group is gloo
+on every host — the same code the CPU tests (world size 2) and the GPU test (2 ranks on one
+device) run; no RCCL communicator is created, because nothing on the data path exchanges."""
 from __future__ import annotations
 
 import os
 import time
 from dataclasses import dataclass
 from typing import Callable
+
+BACKEND = "gloo"
 
 
 @dataclass
@@ -18,23 +22,17 @@ class Rank:
     dist: object = None  # torch.distributed when world > 1
 
 
-def init(backend: str | None = None) -> Rank:
-    """Read RANK/WORLD_SIZE/LOCAL_RANK (torch.distributed.run); init the process group if > 1."""
+def init() -> Rank:
+    """Read RANK/WORLD_SIZE/LOCAL_RANK (torch.distributed.run); init the gloo control-plane group
+    if > 1 rank."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     r = Rank(rank, world, local, None)
     if world > 1:
-        import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group(BACKEND)
         r.dist = dist
     return r
 
@@ -53,8 +51,7 @@ def max_over_ranks(r: Rank, value: float) -> float:
     if r.dist is None:
         return value
     import torch
-    dev = "cuda" if r.dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    t = torch.tensor([value], dtype=torch.float64)
     r.dist.all_reduce(t, op=r.dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -63,8 +60,7 @@ def sum_over_ranks(r: Rank, value: float) -> float:
     if r.dist is None:
         return value
     import torch
-    dev = "cuda" if r.dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    t = torch.tensor([value], dtype=torch.float64)
     r.dist.all_reduce(t, op=r.dist.ReduceOp.SUM)
     return float(t.item())
 

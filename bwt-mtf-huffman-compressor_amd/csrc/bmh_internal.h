@@ -96,7 +96,7 @@ struct Ctx {
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     static constexpr int kStageSlots = 3;  // host-buffer streaming: batches in flight (H2D / encode / D2H)
     uint8_t *stage_in[kStageSlots] = {}, *stage_out[kStageSlots] = {};
-    size_t stage_in_size = 0, stage_out_size = 0;
+    size_t stage_in_size[kStageSlots] = {}, stage_out_size[kStageSlots] = {};  // per slot, allocated on first use
 
     void *get(Slot s, size_t bytes);
     void *host_pinned(size_t bytes);

@@ -250,14 +250,8 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     }
     std::vector<uint32_t> cut(S + 1, nb);
     cut[0] = 0;
-    // BMH_SPLIT (experiments): percent of the batch in run 0 when there are two runs
-    static const int split_pct = [] {
-        const char *e = getenv("BMH_SPLIT");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 && v < 100 ? v : 0;
-    }();
     for (int s = 1; s < S; ++s) {
-        const uint64_t target = (S == 2 && split_pct) ? bt.total * (uint64_t)split_pct / 100 : bt.total * s / S;
+        const uint64_t target = bt.total * s / S;
         uint32_t b = cut[s - 1] + 1;
         while (b < nb - (uint32_t)(S - s) && bt.offs[b] < target) ++b;
         cut[s] = b;
@@ -359,41 +353,53 @@ static unsigned copy_threads()
     return std::min(16u, hw);
 }
 
-// Page-locked (hipHostMalloc'd or hipHostRegister'ed) host range: the DMA engines read and
-// write it directly, so the streaming encoder skips its staging copies.
-static bool is_pinned(const void *p, uint64_t bytes)
+// Page-locked (hipHostMalloc'd or hipHostRegister'ed) host range that device `dev`'s DMA engines
+// may read and write directly, so the streaming encoder skips its staging copies. The range is
+// probed at both ends and every 64 MiB in between (a range over two pinned allocations with an
+// unpinned gap fails the probe in the gap unless the gap is < 64 MiB; callers pass one
+// allocation). Memory registered for another device counts only when it is portable.
+static bool is_pinned(const void *p, uint64_t bytes, int dev)
 {
     if (!p || bytes == 0) return false;
-    for (const uint8_t *q : {(const uint8_t *)p, (const uint8_t *)p + bytes - 1}) {
+    const uint8_t *b = (const uint8_t *)p;
+    constexpr uint64_t kStride = 64ull << 20;
+    for (uint64_t off = 0;; off = std::min(off + kStride, bytes - 1)) {
         hipPointerAttribute_t a;
-        if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+        if (hipPointerGetAttributes(&a, b + off) != hipSuccess) {
             (void)hipGetLastError();
             return false;
         }
         if (a.type != hipMemoryTypeHost) return false;
+        if (off == 0 && a.device != dev) {
+            unsigned int fl = 0;
+            if (hipHostGetFlags(&fl, (void *)b) != hipSuccess) {
+                (void)hipGetLastError();
+                return false;
+            }
+            if (!(fl & hipHostMallocPortable)) return false;
+        }
+        if (off == bytes - 1) return true;
     }
-    return true;
 }
 
-static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes)
+// Page-locked staging for the first `ns` slots, each direction only when it is used (a pinned
+// caller buffer needs none) and sized to the call's largest batch: a slot grows, never shrinks,
+// and is released with the context.
+static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes, int ns)
 {
     if (!c->s_h2d) BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
     if (!c->s_d2h) BMH_HIP(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
-    if (c->stage_in_size < in_bytes) {
-        for (auto &p : c->stage_in) {
-            if (p) BMH_HIP(hipHostFree(p));
-            p = nullptr;
-        }
-        for (auto &p : c->stage_in) BMH_HIP(hipHostMalloc((void **)&p, in_bytes, hipHostMallocDefault));
-        c->stage_in_size = in_bytes;
-    }
-    if (c->stage_out_size < out_bytes) {
-        for (auto &p : c->stage_out) {
-            if (p) BMH_HIP(hipHostFree(p));
-            p = nullptr;
-        }
-        for (auto &p : c->stage_out) BMH_HIP(hipHostMalloc((void **)&p, out_bytes, hipHostMallocDefault));
-        c->stage_out_size = out_bytes;
+    auto grow = [](uint8_t *&p, size_t &have, size_t need) {
+        if (need == 0 || have >= need) return;
+        if (p) BMH_HIP(hipHostFree(p));
+        p = nullptr;
+        have = 0;
+        BMH_HIP(hipHostMalloc((void **)&p, need, hipHostMallocDefault));
+        have = need;
+    };
+    for (int s = 0; s < ns; ++s) {
+        grow(c->stage_in[s], c->stage_in_size[s], in_bytes);
+        grow(c->stage_out[s], c->stage_out_size[s], out_bytes);
     }
 }
 
@@ -456,11 +462,11 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
         max_in = std::max(max_in, bt.offs.back());
         max_cap = std::max(max_cap, bt.cap);
     }
-    ensure_staging(c, in_pinned ? 1 : max_in, pout ? 1 : max_cap);
     std::vector<uint8_t *> dst(K, nullptr);  // pinned destination of each batch's records
     // kStageSlots batches in flight: the H2D of batch k waits only for the encode of k - NS
     constexpr int NS = Ctx::kStageSlots;
-    const int ns = (int)std::min<size_t>(NS, K);
+    const int ns = (int)std::min<size_t>(NS, K);  // slots k % NS for k < K
+    ensure_staging(c, in_pinned ? 0 : max_in, pout ? 0 : max_cap, ns);
     const Slot ws_in[NS] = {WS_IN, WS_IN2, WS_IN3}, ws_out[NS] = {WS_OUT, WS_OUT2, WS_OUT3};
     uint8_t *d_in[NS] = {}, *d_out[NS] = {};
     for (int s = 0; s < ns; ++s) {
@@ -794,7 +800,7 @@ bmh_status bmh_host_alloc(bmh_ctx *c, uint64_t bytes, void **h_ptr)
 bmh_status bmh_host_free(bmh_ctx *c, void *h_ptr)
 {
     API_BEGIN
-    use_device(c);
+    if (c) use_device(c);
     if (h_ptr) BMH_HIP(hipHostFree(h_ptr));
     API_END
 }
@@ -934,7 +940,10 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
     const bool direct = nctx == 1;
     const uint64_t table = nblocks == 1 ? 0 : 32 + 8 * nblocks;
     use_device(ctxs[0]);
-    const bool in_pinned = is_pinned(in, n), out_pinned = direct && is_pinned(out, out_cap);
+    // the DMA-only paths, decided per context device (several contexts may sit on other GPUs)
+    std::vector<char> in_pinned(nctx);
+    for (uint32_t g = 0; g < nctx; ++g) in_pinned[g] = is_pinned(in, n, ctxs[g]->device);
+    const bool out_pinned = direct && is_pinned(out, out_cap, ctxs[0]->device);
     uint64_t at = table;
     if (direct && table > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
     std::vector<bmh_status> st(nctx, BMH_OK);
@@ -956,7 +965,7 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
                         }
                         at += bytes;
                     },
-                    in_pinned, out_pinned ? &po : nullptr);
+                    in_pinned[g] != 0, out_pinned ? &po : nullptr);
             } else {
                 encode_host_blocks(ctxs[g], in, n, bs, bl,
                                    [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
@@ -967,7 +976,7 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
                                            recs[bl[i0 + i]] = RecRef{buf.get() + ro[i], ro[i + 1] - ro[i]};
                                        store[g].push_back(std::move(buf));
                                    },
-                                   in_pinned);
+                                   in_pinned[g] != 0);
             }
         } catch (const Error &e) {
             st[g] = e.status;

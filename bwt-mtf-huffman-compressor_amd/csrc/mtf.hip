@@ -24,6 +24,8 @@
 //                tools/microbench/mtf_variants.hip).
 //   4. hist    : freq + first occurrence of each MTF value per block (LDS atomics).
 #include "bmh_internal.h"
+
+#include <atomic>
 #include "device_util.h"
 
 #include <algorithm>
@@ -54,9 +56,13 @@ static uint32_t mtf_chunk_len(int device, uint64_t total)
     uint64_t x = env;
     if (!x && total > kMtfAdaptiveMax) x = kMtfChunk;
     if (!x) {
-        static int cus[64] = {};
-        int &cu = cus[device & 63];
-        if (!cu && hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cu = 256;
+        // per-device CU count, cached (host threads of several contexts call this concurrently)
+        static std::atomic<int> cus[64] = {};
+        int cu = cus[device & 63].load(std::memory_order_relaxed);
+        if (!cu) {
+            if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cu = 256;
+            cus[device & 63].store(cu, std::memory_order_relaxed);
+        }
         const uint64_t lanes = (uint64_t)std::max(cu, 1) * 6 * 64;
         x = std::max<uint64_t>(kMtfChunkMin, (total + lanes - 1) / lanes);
     }

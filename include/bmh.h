@@ -62,7 +62,9 @@ void *bmh_ctx_stream(bmh_ctx *ctx);
 bmh_status bmh_dev_alloc(bmh_ctx *ctx, uint64_t bytes, void **d_ptr);
 bmh_status bmh_dev_free(bmh_ctx *ctx, void *d_ptr);
 /* Page-locked host memory (hipHostMalloc). bmh_compress_host detects page-locked input and
- * output buffers and then moves the data by DMA only: no staging copies on the host. */
+ * output buffers and then moves the data by DMA only: no staging copies on the host.
+ * The block is not tied to the context: bmh_host_free accepts ctx == NULL (e.g. after the
+ * context that allocated it was destroyed). */
 bmh_status bmh_host_alloc(bmh_ctx *ctx, uint64_t bytes, void **h_ptr);
 bmh_status bmh_host_free(bmh_ctx *ctx, void *h_ptr);
 bmh_status bmh_memcpy_h2d(bmh_ctx *ctx, void *d_dst, const void *h_src, uint64_t bytes);

@@ -35,7 +35,7 @@ def _worker(rank, world, port, q):
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
     from oracle_ffi import Oracle
-    r = dist.init("gloo")
+    r = dist.init()
     try:
         orc = Oracle()
         blocks = _blocks()
@@ -90,7 +90,7 @@ def _bench_worker(rank, world, port, q, scaling):
     sys.path.insert(0, here)
     sys.path.insert(0, os.path.dirname(here))
     import bench
-    r = dist.init("gloo")
+    r = dist.init()
     try:
         bs = 1 << 22
         # strong: 2 blocks in total dealt over the ranks; weak: 1 block per rank

@@ -1,8 +1,11 @@
 """GPU: bench.py's N-rank path with the real libbmh encoder — 2 ranks under
-torch.distributed.run sharing the test box's GPU (BMH_DIST_BACKEND=gloo: ranks map to
-device local_rank mod device_count; the process group carries only the barriers and the
-max-over-ranks / sum-over-ranks reductions, never block data). Each rank checks its own
-records against the reference manifest (config 4, SURVEY §8e: block b -> rank b mod N).
+torch.distributed.run sharing the test box's GPU, launched exactly as the driver launches the
+scaling runs (ranks map to device local_rank mod device_count; the gloo process group carries
+only the barriers and the max-over-ranks / sum-over-ranks reductions, never block data — the
+same control plane as on 8 GPUs, bmh/dist.py). Each rank checks its own records against the
+reference manifest (config 4, SURVEY §8e: block b -> rank b mod N); the weak case also runs
+the default line's decode, PCIe-inclusive and Calgary legs, so every leg of the driver's N > 1
+line has run under a test.
 
 The ranks are started as child processes of this (GPU-initialised) pytest process; nothing
 here replaces a running program."""
@@ -28,13 +31,14 @@ def _free_port() -> int:
 @pytest.mark.gpu
 @pytest.mark.parametrize("scaling", ["weak", "strong"])
 def test_world2_bench_on_gpu(scaling):
-    env = dict(os.environ, BMH_DIST_BACKEND="gloo")
+    env = dict(os.environ)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling, "--no-cpu-baseline",
-           "--decode-steps", "0", "--pcie-steps", "0", "--calgary-steps", "0"]
-    if scaling == "weak":
-        cmd += ["--bytes-per-gpu", str(256 << 20)]  # 64 blocks per rank
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling]
+    if scaling == "weak":  # 64 blocks per rank, every leg of the default line
+        cmd += ["--bytes-per-gpu", str(256 << 20), "--decode-steps", "1", "--pcie-steps", "1", "--calgary-steps", "1"]
+    else:
+        cmd += ["--decode-steps", "0", "--pcie-steps", "0", "--calgary-steps", "0"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.strip().splitlines() if x.startswith("{")][-1])
@@ -42,3 +46,9 @@ def test_world2_bench_on_gpu(scaling):
     assert line["value"] > 0 and line["ms_per_step"] > 0
     nblk = 128 if scaling == "weak" else 256  # blocks over both ranks
     assert line["parity"] == f"{nblk}/{nblk} records byte-identical to the reference manifest", line["parity"]
+    assert line["cpu_baseline"] is None  # N > 1: the CPU baseline is an N = 1 leg
+    if scaling == "weak":
+        assert line["decode"]["roundtrip_bit_exact"]
+        assert line["pcie_inclusive"]["records_equal_device_encode"]
+        assert line["calgary"]["whole_files"]["records_byte_identical_to_reference"]
+        assert line["calgary"]["blocks_256k"]["records_byte_identical_to_reference"]

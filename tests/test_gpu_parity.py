@@ -583,6 +583,31 @@ def test_compress_host_multi_matches_single_context(ctx):
             c.close()
 
 
+def test_compress_host_multi_distinct_devices(ctx):
+    """bmh_compress_host_multi with one context on EACH visible GPU (the in-process form of the
+    round-robin deal over 1-8 GPUs): same container as one context, with pageable
+    and with page-locked input (the pinned fast path must hold for contexts on other devices
+    than the one the buffer was registered on). Skipped on a one-GPU box: the shared-device
+    case is test_compress_host_multi_matches_single_context."""
+    ndev = int(bmh.lib().bmh_device_count())
+    if ndev < 2:
+        pytest.skip(f"{ndev} GPU visible: distinct-device contexts need >= 2 (the shared-device case runs above)")
+    data = synth.zipf_text(9_000_007).tobytes()
+    ctxs = [ctx] + [bmh.Context(d) for d in range(1, min(ndev, 8))]
+    hin = ctx.alloc_host(len(data))
+    hin.a[:] = np.frombuffer(data, np.uint8)
+    try:
+        for bs in (1 << 20, 3 << 20):
+            single = ctx.compress_bytes(data, block_size=bs)
+            assert bmh.compress_bytes_multi(ctxs, data, bs) == single, bs
+            assert bmh.compress_bytes_multi(ctxs, hin.a, bs) == single, bs
+        assert ctx.decompress_bytes(single) == data
+    finally:
+        hin.free()
+        for c in ctxs[1:]:
+            c.close()
+
+
 def test_cli_compress_matches_reference_binary(tmp_path):
     """`bmh_compress <in> <out>` (the reference's COMPRESS binary, main.cpp:439-447) on the GPU:
     every Calgary record byte-identical to the reference's and its stdout line the same;
@@ -651,7 +676,9 @@ def test_checked_build_full_exec():
     import json
     import subprocess
     import sys
-    chk = os.path.join(os.path.dirname(bmh.LIB_PATH), "..", "lib_check", "libbmh.so")
+    # the in-tree checked build, whatever library BMH_LIB points the rest of the suite at
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    chk = os.path.join(repo, "bwt-mtf-huffman-compressor_amd", "lib_check", "libbmh.so")
     assert os.path.exists(chk), "lib_check/libbmh.so not built (make -C bwt-mtf-huffman-compressor_amd check)"
     env = dict(os.environ, BMH_LIB=os.path.abspath(chk))
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "check_workload.py")], env=env,
