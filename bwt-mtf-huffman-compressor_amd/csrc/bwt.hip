@@ -6,16 +6,19 @@
 // is still tied:
 //
 // Data phase (no rank arrays touched):
-//   global pass : counting sort of every position by the first 12 bits of its rotation
-//                 (4096 buckets per block; LDS histograms; chunks of one block mapped to one
-//                 XCD so the block's bytes and SA write frontier stay in that XCD's L2).
-//   finish      : one workgroup per bucket of <= 4096 positions (bit depth db): LDS counting
-//                 sort by the next 8 bits, then every sub-bucket of <= 64 is ordered by the
-//                 next 32 bits by rank counting (bit depth db + 40). Resolved slots get their
-//                 SA entry AND their last-column byte L[r] = data[(SA[r]+n-1) mod n] here.
-//                 Bigger sub-buckets are deferred to another finish pass at db + 8.
-//   MSD passes  : buckets / sub-buckets larger than 4096 are split by 8 more bits per global
-//                 pass (tile histograms, per-segment scan, scatter) until they fit.
+//   global pass : counting sort of every position by the first kG1Bits = 10 rotation bits
+//                 (1024 buckets per block; LDS histograms per 16 K chunk; chunks of one block
+//                 mapped to one XCD so the block's bytes and record write frontier stay in that
+//                 XCD's L2). Every rotation of a dense bucket leaves an 8-byte record: its next
+//                 12 + R rotation bits, its position and its last-column byte (rec_rbits).
+//   dense finish: one workgroup per bucket of <= 4608 rotations: LDS counting sort by the next
+//                 12 bits, then every sub-bucket of <= 64 is ordered by the next R bits by rank
+//                 counting (R = 22 for 4 MiB blocks: bit depth 44). Resolved slots get their L
+//                 byte (and SA where a later pass reads it). Longer sub-buckets, and rotations
+//                 still tied, are deferred to list passes.
+//   list passes : deferred segments by size: tiny (<= 64, wave shuffles), bitonic (<= 4096, 64
+//                 more rotation bits per round), counting-sort finish (12-bit digit + 32-bit
+//                 ranks) and MSD passes (8 bits past the shared prefix) for longer ones.
 // Doubling phase (only blocks that still hold tied groups, e.g. text or periodic input):
 //   lazy rank fill: rank[p] = slot of p, or its group's start slot (ranks = #strictly smaller
 //   rotations at the current depth); then rounds sorting each tied group by

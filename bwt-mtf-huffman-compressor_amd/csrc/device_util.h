@@ -66,6 +66,19 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t *ctr)
     return base + rank;
 }
 
+// Raw buffer loads: a buffer resource over [p, p + bytes), and loads by 32-bit byte offset
+// whose out-of-range lanes read 0 (the hardware bounds check: no branch, no clamp, and no
+// 64-bit address registers per load). The whole offset is in the VGPR operand (the SGPR
+// offset is not part of the range check).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint64_t buf_load_u64(__amdgpu_buffer_rsrc_t r, uint32_t byte_off)
+{
+    return __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(r, (int)byte_off, 0, 0));
+}
+
 // Inclusive wave64 scans.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x)
 {
