@@ -37,12 +37,25 @@ namespace {
 
 // ---------------------------------------------------------------------------- constants
 constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass workgroup (LDS-staged)
-constexpr uint32_t kG1Bits = 10;                // global-pass digit: first byte + 2 bits
+#ifndef BMH_G1_BITS
+#define BMH_G1_BITS 10
+#endif
+constexpr uint32_t kG1Bits = BMH_G1_BITS;       // global-pass digit: first byte + (kG1Bits - 8) bits
 constexpr uint32_t kG1Bins = 1u << kG1Bits;
 constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passes
 constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // finish workgroup shapes: dense (global-pass buckets), list small, list big
-constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
+// Dense finish of the global pass's buckets: 10-bit pass -> k_finish_dense (<= 4608 rotations,
+// 12-bit digit, R-bit rests); 9-bit pass -> k_finish_wide (<= 9216, 13-bit digit, 16-bit rests).
+// List segments over kFinCap take the counting-sort finish up to kSegCap (large batches) or the
+// batch's big cap, MSD passes beyond.
+constexpr bool kWide = kG1Bits == 9;
+#ifndef BMH_WIDE_NT
+#define BMH_WIDE_NT 1024
+#endif
+constexpr uint32_t kDenseNT = kWide ? BMH_WIDE_NT : 512, kDenseCap = kWide ? 9216 : 4608, kDenseDig = kWide ? 13 : 12;
+constexpr uint32_t kSegNT = 512, kSegCap = 4608;
+static_assert(kG1Bits == 9 || kG1Bits == 10, "global-pass digit");
 constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register bitonic sort
 // List segments longer than the batch's big cap take MSD passes (8 bits past their shared prefix
 // per pass); shorter ones over kFinCap a counting-sort finish (12-bit digit + 32-bit ranks).
@@ -52,7 +65,7 @@ constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register b
 // which resolves 44 bits per round where an MSD pass takes 8 (half the rounds).
 constexpr uint32_t kBigCapLarge = 4096, kBigCapSmall = 19072, kBigNT = 1024;
 constexpr uint64_t kBigCapLargeBatch = 8ull << 20;  // batches of more bytes use kBigCapLarge
-static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kDenseCap, "list classes");
+static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kSegCap && kSegCap <= kDenseCap, "list classes");
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
 constexpr uint32_t kDataMaxBits = 512;          // deeper MSD ties go to rank doubling
@@ -85,7 +98,7 @@ constexpr uint32_t kRunMode = 1u << 30;
 #endif
 constexpr uint32_t kMsdBits = BMH_MSD_BITS, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
 static_assert(kMsdBins >= 65 && kMsdBins <= 1024, "MSD digit (run-mode digits 0..64)");
-constexpr uint32_t kWinShift = 16, kG1WinBits = 54;
+constexpr uint32_t kWinShift = 16, kG1WinBits = 64 - kG1Bits;
 __device__ __forceinline__ uint32_t seg_known(uint32_t w) { return (w >> kWinShift) & 127u; }
 
 struct Counters {
@@ -222,7 +235,8 @@ __device__ __forceinline__ uint32_t defer_list(const DataArgs &a, Seg4 &sg, uint
         a.cnt->flagged = 1;
         return kListGroups;
     }
-    return sg.y <= kTinyFin ? kListTiny : sg.y <= kFinCap ? kListFin : kListFinb;
+    if (sg.y > kFinCap) return sg.y > a.big_cap && sg.y > kSegCap ? kListBig : kListFinb;
+    return sg.y <= kTinyFin ? kListTiny : kListFin;
 }
 
 // Deferred segments queued per workgroup in LDS; one global atomic per list reserves the
@@ -308,6 +322,10 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
 // finish resolves rotation bits up to 44; rarer deeper ties go to list passes).
 __device__ __forceinline__ uint32_t rec_pbits(uint32_t n) { return n <= 2 ? 1u : 32u - (uint32_t)__builtin_clz(n - 1); }
 __device__ __forceinline__ uint32_t rec_rbits(uint32_t P) { return min(32u, 44u - P); }
+// The wide finish's record (kG1Bits = 9) needs no decoding: high dword = rotation bits
+// [9, 9 + kRecKeyBits) (its 13-bit digit << 16 | 16-bit rest), low dword = p << 8 | L (blocks
+// of <= 16 MiB) or p (the finish gathers L).
+constexpr uint32_t kRecKeyBits = kDenseDig + 16;
 
 // ------------------------------------------------------------------------- global pass
 // Counting sort of every block by its first kG1Bits rotation bits. Chunks of <= 16 K
@@ -476,9 +494,15 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     const uint32_t t = threadIdx.x;
     const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint8_t *blk = a.data + boff;
-    static_assert(kG1Bins == 1024, "one digit per thread");
+    static_assert(kG1Bins <= 1024 && kG1Bits >= 8, "at most one digit per thread");
+    const bool tdig = kG1Bins == 1024 || t < kG1Bins;  // this thread owns digit t
+    const bool packL = rec_pbits(n) <= 24;              // (wide records carry the L byte)
     // the chunk's digit offsets and bucket sizes: loads issued together with the text's
-    const uint32_t cv = chist[(size_t)blockIdx.x * kG1Bins + t], bl = bk[(size_t)b * kG1Bins + t].y;
+    uint32_t cv = 0, bl = 0;
+    if (tdig) {
+        cv = chist[(size_t)blockIdx.x * kG1Bins + t];
+        bl = bk[(size_t)b * kG1Bins + t].y;
+    }
     {
         // 16-byte pieces, all loads in flight before the first LDS store (a load under a
         // per-piece branch waits inside it: one HBM round trip per piece); pieces that wrap
@@ -511,9 +535,11 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
             *(uint4 *)&s_txt[4 * pc] = v[j];
         }
     }
-    s_cnt[t] = 0;
-    s_off[t] = cv;
-    s_blen[t] = bl;
+    if (tdig) {
+        s_cnt[t] = 0;
+        s_off[t] = cv;
+        s_blen[t] = bl;
+    }
     GPROF(5);
     __syncthreads();
     GPROF(0);
@@ -539,9 +565,11 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     __syncthreads();
     GPROF(1);
     {
-        const uint32_t ex = block_excl_sum1<1024>(s_cnt[t], s_tmp);
-        s_off[t] -= ex;  // slot of local element i with digit d = s_off[d] + i
-        s_cnt[t] = ex;
+        const uint32_t ex = block_excl_sum1<1024>(tdig ? s_cnt[t] : 0u, s_tmp);
+        if (tdig) {
+            s_off[t] -= ex;  // slot of local element i with digit d = s_off[d] + i
+            s_cnt[t] = ex;
+        }
     }
     __syncthreads();
     GPROF(2);
@@ -569,14 +597,19 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint32_t slot = s_off[d] + i;
         const uint32_t blen = s_blen[d];
         if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
-            const uint32_t P = rec_pbits(n), R = rec_rbits(P);
-            const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
-            rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
+            if constexpr (kWide) {
+                const uint64_t k = (key << (kG1Bits - 8)) >> (64 - kRecKeyBits);
+                rec[boff + slot] = (k << 32) | (packL ? (p << 8) | (uint32_t)(key & 255u) : p);
+            } else {
+                const uint32_t P = rec_pbits(n), R = rec_rbits(P);
+                const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
+                rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
+            }
         } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
             // a bucket for the MSD passes: its first pass reads rotation bits [10, 64) from here
-            // (MSB-aligned, low 10 bits zero) instead of gathering them (kG1WinBits known)
-            if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << 2) & ~0x3ffull;
+            // (MSB-aligned, low kG1Bits bits zero) instead of gathering them (kG1WinBits known)
+            if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << (kG1Bits - 8)) & ~(uint64_t)(kG1Bins - 1);
         }
         if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
@@ -1196,6 +1229,185 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     __syncthreads();
     DPROF(0);
     finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+}
+
+// Wide dense finish for kG1Bits = 9 (buckets of ~8192 rotations on random data; the global
+// pass then writes its records in per-digit runs of ~32, half as many cache-line pieces as with
+// 10 bits). 512 threads x IPT elements, kept in two registers each (record = digit << 16 | rest,
+// and p << 8 | L or p: nothing to decode); a DIG-bit LDS counting sort with 16-bit counters, then
+// every element ranks itself inside its sub-bucket by the 16-bit rest (rotation bits up to
+// kG1Bits + DIG + 16). 16-bit rests keep the LDS at < 40 KB: four workgroups per CU. Final slots
+// are parked as L bytes (over the dead counters) and stored in slot order; SA is stored only for
+// the slots a later pass reads (deferred sub-buckets, tie groups) or in full-SA mode.
+template <uint32_t NT, uint32_t CAP, uint32_t DIG>
+__global__ __launch_bounds__(NT) void k_finish_wide(DataArgs a, const uint2 *__restrict__ bk,
+                                                    const uint64_t *__restrict__ rec)
+{
+    constexpr uint32_t IPT = (CAP + NT - 1) / NT;
+    constexpr uint32_t NDIG = 1u << DIG, NW = NDIG / 2, WPT = NW / NT;  // counter words (2 digits each)
+    constexpr uint32_t DMASK = NDIG - 1, KEEP = 1u << 31;
+    static_assert(DIG + 16 == kRecKeyBits && WPT % 4 == 0 && CAP <= 4 * NW && CAP < (1u << (31 - DIG)), "wide shape");
+    __shared__ uint16_t s_rest[CAP + 4];
+    __shared__ __align__(16) uint32_t s_cnt[NW];  // digit counters; then the parked L bytes
+    __shared__ uint32_t s_tmp[NT / 64 + 1];
+    __shared__ DeferQueue<kDeferQ> dq;
+    uint8_t *const s_park = reinterpret_cast<uint8_t *>(s_cnt);
+    const uint32_t x = blockIdx.x & 7u, kb = blockIdx.x >> 3;
+    const uint32_t b = x + 8u * (kb >> kG1Bits);
+    if (b >= a.nb) return;
+    const uint2 e = bk[(size_t)b * kG1Bins + (kb & (kG1Bins - 1))];
+    const uint32_t len = e.y;
+    if (len < 2 || len > CAP) return;
+    const uint32_t t = threadIdx.x;
+    DPROF_START;
+    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff, gstart = boff + e.x;
+    const bool packL = rec_pbits(n) <= 24;
+    const uint8_t *blk = a.data + boff;
+    // records: every load in flight before the first is used (slots past the bucket read 0)
+    const __amdgpu_buffer_rsrc_t rs = make_rsrc(rec + gstart, len * 8u);
+    uint32_t pl[IPT], dd[IPT];
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint64_t r = buf_load_u64(rs, (t + k * NT) * 8u);
+        dd[k] = (uint32_t)(r >> 32);
+        pl[k] = (uint32_t)r;
+    }
+    for (uint32_t i = t; i < NW; i += NT) s_cnt[i] = 0;
+    if (t == 0) s_tmp[NT / 64] = 0;
+    dq_init(dq);
+    __syncthreads();
+    DPROF(0);
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t d = dd[k] >> 16;
+        if (t + k * NT < len) atomicAdd(&s_cnt[d >> 1], 1u << (16 * (d & 1u)));
+    }
+    __syncthreads();
+    DPROF(1);
+    {
+        // thread t owns counter words WPT*t .. WPT*t + WPT - 1 (read 16 bytes at a time):
+        // counts -> starts
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < WPT; j += 4) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(&s_cnt[WPT * t + j]);
+            sum += (w.x & 0xffffu) + (w.x >> 16) + (w.y & 0xffffu) + (w.y >> 16) + (w.z & 0xffffu) + (w.z >> 16) +
+                   (w.w & 0xffffu) + (w.w >> 16);
+        }
+        uint32_t ex = block_excl_sum1<NT>(sum, s_tmp);
+#pragma unroll
+        for (uint32_t j = 0; j < WPT; j += 4) {
+            uint4 w = *reinterpret_cast<const uint4 *>(&s_cnt[WPT * t + j]);
+            uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t e0 = ex, e1 = ex + (v[q] & 0xffffu);
+                ex = e1 + (v[q] >> 16);
+                v[q] = e0 | (e1 << 16);
+            }
+            *reinterpret_cast<uint4 *>(&s_cnt[WPT * t + j]) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+    }
+    __syncthreads();
+    DPROF(2);
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        if (t + k * NT < len) {
+            // (an opaque copy: the counting pass's address and shift are recomputed here, not kept
+            // live in registers per element from there)
+            uint32_t h = dd[k];
+            asm volatile("" : "+v"(h));
+            const uint32_t d = h >> 16, sh = 16 * (d & 1u);
+            const uint32_t me = (atomicAdd(&s_cnt[d >> 1], 1u << sh) >> sh) & 0xffffu;
+            s_rest[me] = (uint16_t)h;
+            dd[k] = d | (me << DIG);
+        }
+    }
+    __syncthreads();
+    DPROF(3);
+    // s_cnt now holds every sub-bucket's end; its start is the previous digit's end
+    const uint64_t newbits = (uint64_t)kG1Bits + DIG + 16;
+    const bool final_depth = newbits >= 8ull * n;
+    const bool full_sa = a.full_sa != 0;
+    auto bound_words = [&](uint32_t k, uint32_t &w0, uint32_t &w1) {
+        const uint32_t d = t + k * NT < len ? dd[k] & DMASK : 0u;
+        w1 = s_cnt[d >> 1];
+        w0 = s_cnt[((d - 1) >> 1) & (NW - 1)];
+    };
+    uint32_t nw0, nw1;
+    bound_words(0, nw0, nw1);
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        const uint32_t w0 = nw0, w1 = nw1;
+        if (k + 1 < IPT) bound_words(k + 1, nw0, nw1);
+        if (t + k * NT >= len) continue;
+        const uint32_t d = dd[k] & DMASK, me = dd[k] >> DIG;
+        const uint32_t p = packL ? pl[k] >> 8 : pl[k];
+        const uint32_t s1 = (w1 >> (16 * (d & 1u))) & 0xffffu;
+        const uint32_t s0 = d ? (w0 >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
+        const uint32_t m = s1 - s0;
+        if (m > kSmallM) {  // deferred whole, grouped by the digit (its SA is read later)
+            dd[k] = me | KEEP;
+            if (me == s0) dq_push(a, dq, gstart + s0, m, kG1Bits + DIG, b, n);
+            continue;
+        }
+        // rank = #(rest, slot) pairs below this element's; the first four members read together
+        // (m <= 4 for ~99 % of the sub-buckets on random data; this element's own rest is one
+        // of them then), the rest one by one
+        uint32_t c = 0, eqt = 1, r;
+        if (m > 1) {
+            uint32_t rf4[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                rf4[j] = 0;
+                if (j < 2 || s0 + j < s1) rf4[j] = s_rest[s0 + j];
+            }
+            const uint32_t o = me - s0;
+            r = o == 0 ? rf4[0] : o == 1 ? rf4[1] : o == 2 ? rf4[2] : o == 3 ? rf4[3] : (uint32_t)s_rest[me];
+            const uint32_t key = (r << 16) | me;
+            eqt = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) {
+                const bool in = s0 + j < s1;
+                c += in && ((rf4[j] << 16) | (s0 + j)) < key;
+                eqt += in && rf4[j] == r;
+            }
+#pragma nounroll
+            for (uint32_t f = s0 + 4; f < s1; ++f) {
+                const uint32_t rf = s_rest[f];
+                c += ((rf << 16) | f) < key;
+                eqt += rf == r;
+            }
+        }
+        const uint32_t local = s0 + c;
+        uint32_t gs = local;
+        bool keep = full_sa;
+        if (eqt > 1) {  // tied so far: the group starts after the strictly smaller rests
+            uint32_t lt = 0;
+            for (uint32_t f = s0; f < s1; ++f) lt += s_rest[f] < r;
+            gs = s0 + lt;
+            keep = true;
+            if (c == lt) dq_push(a, dq, gstart + gs, eqt, (uint32_t)newbits, b, n);
+        }
+        dd[k] = local | (keep ? KEEP : 0u);
+        if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = e.x + gs;
+    }
+    DPROF(4);
+    dq_flush<NT>(a, dq);  // (starts with a barrier: the counters are dead after it)
+    DPROF(5);
+    // slot -> L byte (SA stored here for the slots a later pass reads)
+#pragma unroll
+    for (uint32_t k = 0; k < IPT; ++k) {
+        if (t + k * NT < len) {
+            const uint32_t slot = dd[k] & ~KEEP, p = packL ? pl[k] >> 8 : pl[k];
+            s_park[slot] = packL ? (uint8_t)pl[k] : lastcol_byte(blk, n, p);
+            if (dd[k] & KEEP) a.sa[gstart + slot] = p;
+        }
+    }
+    __syncthreads();
+    DPROF(6);
+    for (uint32_t i = t; i < len; i += NT) a.L[gstart + i] = s_park[i];
+    DPROF(7);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -2221,8 +2433,12 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
-        BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
-                   da, bk, rec);
+        if constexpr (kWide)
+            BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_wide<kDenseNT, kDenseCap, kDenseDig>), 8u * cdiv(nb, 8) * kG1Bins,
+                       kDenseNT, 0, da, bk, rec);
+        else
+            BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<512, 4608>), 8u * cdiv(nb, 8) * kG1Bins, 512, 0, da, bk,
+                       rec);
 #if defined(BMH_PROF_SCATTER) || defined(BMH_PROF_DENSE)
         {
             std::vector<uint32_t> h((1u << 18) * 8);
@@ -2330,11 +2546,11 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
                                lm[kListFin]);
             }
             if (tot[kListFinb]) {  // counting-sort finish: dense shape, or 1024 threads up to kBigCapSmall
-                if (big_cap > kDenseCap)
+                if (big_cap > kSegCap)
                     BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kBigNT, kBigCapSmall>), 8u * rows[kListFinb], kBigNT, 0,
                                da, lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
                 else
-                    BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kDenseNT, kDenseCap>), 8u * rows[kListFinb], kDenseNT, 0,
+                    BMH_LAUNCH(c, "bwt_finish_big", (k_finish_seg<kSegNT, kSegCap>), 8u * rows[kListFinb], kSegNT, 0,
                                da, lb[in], d_loff + kListFinb * 9, dc + kListFinb * 8, kFinCap, lm[kListFinb]);
             }
             if (tot[kListBig]) {
