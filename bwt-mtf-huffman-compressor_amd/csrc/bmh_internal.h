@@ -57,6 +57,7 @@ enum Slot : int {
 
 struct Ctx {
     int device = 0;
+    int cus = 256;  // compute units of the device (persistent-grid sizing)
     hipStream_t stream = nullptr;
     bool timing = false;
     std::map<std::string, KStat> stats;

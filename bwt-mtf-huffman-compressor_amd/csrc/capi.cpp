@@ -216,6 +216,7 @@ static Ctx *sub_ctx(Ctx *c, size_t i)
     while (c->subs.size() <= i) {
         Ctx *x = new bmh_ctx();
         x->device = c->device;
+        x->cus = c->cus;
         if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
             delete x;
             fail(BMH_EHIP, "stream creation failed");
@@ -726,6 +727,7 @@ bmh_status bmh_ctx_create(int device, bmh_ctx **out)
     BMH_HIP(hipSetDevice(device));
     bmh_ctx *c = new bmh_ctx();
     c->device = device;
+    c->cus = std::max(1, prop.multiProcessorCount);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         fail(BMH_EHIP, "stream creation failed");
