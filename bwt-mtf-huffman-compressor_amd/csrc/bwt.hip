@@ -74,6 +74,7 @@ constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register b
 // which resolves 44 bits per round where an MSD pass takes 8 (half the rounds).
 constexpr uint32_t kBigCapLarge = 4096, kBigCapSmall = 19072, kBigNT = 1024;
 constexpr uint64_t kBigCapLargeBatch = 8ull << 20;  // batches of more bytes use kBigCapLarge
+constexpr uint64_t kFullSaBatch = 16ull << 20;      // batches up to this size store the full SA
 static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kSegCap && kSegCap <= kDenseCap, "list classes");
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
@@ -2709,7 +2710,10 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
     // with every SA entry stored, and the context keeps that mode while its batches need it.
-    bool full_sa = c->bwt_full_sa;
+    // Small (latency-bound) batches store every SA entry from the start: the stores cost a few
+    // microseconds, a re-run of the data phase (when a block turns out to need rank doubling,
+    // e.g. Calgary's pic on a fresh context) costs milliseconds.
+    bool full_sa = c->bwt_full_sa || N <= kFullSaBatch;
     uint64_t *kb_cur = rec, *kb_nxt = nullptr;  // MSD window buffers (see the big-list passes)
     for (;;) {
         da.full_sa = full_sa ? 1u : 0u;
