@@ -58,11 +58,17 @@ constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
 // 12-bit digit, R-bit rests); 9-bit pass -> k_finish_wide (<= 9216, 13-bit digit, 16-bit rests).
 // List segments over kFinCap take the counting-sort finish up to kSegCap (large batches) or the
 // batch's big cap, MSD passes beyond.
-constexpr bool kWide = kG1Bits == 9;
+#ifndef BMH_DENSE_V2
+#define BMH_DENSE_V2 0
+#endif
+// kWide: the decode-free record layout and k_finish_wide (always with the 9-bit pass; with the
+// 10-bit pass when BMH_DENSE_V2: 4608-rotation buckets, 12-bit digit, 16-bit rests)
+constexpr bool kWide = kG1Bits == 9 || BMH_DENSE_V2;
 #ifndef BMH_WIDE_NT
 #define BMH_WIDE_NT 1024
 #endif
-constexpr uint32_t kDenseNT = kWide ? BMH_WIDE_NT : 512, kDenseCap = kWide ? 9216 : 4608, kDenseDig = kWide ? 13 : 12;
+constexpr uint32_t kDenseNT = kG1Bits == 9 ? BMH_WIDE_NT : 512, kDenseCap = kG1Bits == 9 ? 9216 : 4608,
+                   kDenseDig = kG1Bits == 9 ? 13 : 12;
 constexpr uint32_t kSegNT = 512, kSegCap = 4608;
 static_assert(kG1Bits == 9 || kG1Bits == 10, "global-pass digit");
 constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register bitonic sort
