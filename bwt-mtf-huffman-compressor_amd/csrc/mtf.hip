@@ -70,6 +70,10 @@ static uint32_t mtf_chunk_len(int device, uint64_t total)
     return (uint32_t)((x + 63) & ~63ull);
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
+#ifndef BMH_MTF_AHEAD
+#define BMH_MTF_AHEAD 1
+#endif
+constexpr int kMtfAhead = BMH_MTF_AHEAD;  // symbols whose stamp reads run ahead of the update
 
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
@@ -279,6 +283,80 @@ __device__ __forceinline__ uint32_t mtf_step(uint32_t c, bool valid, uint32_t no
     return r;
 }
 
+// A whole super-group (symbols j = 0..63 at slots now + j), software-pipelined: symbol j + 1's
+// stamp and epoch reads are issued before symbol j's state update, and symbol j's marks / counts
+// reads are consumed only after that update has been issued, so each symbol waits on one LDS
+// round trip that overlaps its neighbours' work instead of two back to back. A read-ahead stamp
+// predates the previous symbol's update, so a symbol equal to its predecessor takes the
+// predecessor's slot (the only stamp that update can change). Same results as mtf_step.
+__device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, uint8_t *s, uint32_t l4, uint32_t &S,
+                                          uint4 (&o4)[4])
+{
+    const uint32_t iw[16] = {in[0].x, in[0].y, in[0].z, in[0].w, in[1].x, in[1].y, in[1].z, in[1].w,
+                             in[2].x, in[2].y, in[2].z, in[2].w, in[3].x, in[3].y, in[3].z, in[3].w};
+    auto sym = [&](int j) { return (iw[j >> 2] >> (8 * (j & 3))) & 255u; };
+    auto a8 = [&](uint32_t c) { return (kRowTm << 8) + ((c >> 2) << 8) + l4 + (c & 3u); };
+    auto ae = [&](uint32_t c) { return (kRowEp << 8) + ((c >> 5) << 8) + l4; };
+    // now is a multiple of 64: the group's marks words are (now >> 5) and the next one, both
+    // counted in one counter row, byte (now >> 5) & 3 (0 or 2) and the byte above
+    const uint32_t bits0 = (kRowBits << 8) + ((now >> 5) << 8) + l4;
+    const uint32_t cnt0 = (kRowCnt << 8) + ((now >> 7) << 8) + l4;
+    const uint32_t inc0 = 1u << (8 * ((now >> 5) & 3u)), sinc = 1u << (8 * (now >> 7));
+    uint32_t ow[16];
+    uint32_t plo[64], pe[64];  // read-ahead stamp bytes / epoch words (registers once unrolled)
+#pragma unroll
+    for (int j = 0; j < kMtfAhead; ++j) {
+        plo[j] = s[a8(sym(j))];
+        pe[j] = lds_u32(s, ae(sym(j)));
+    }
+    uint32_t pbw = 0, pcw = 0, pt = 0, psw = 0, pr = 0;  // the previous symbol's deferred rank terms
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        const uint32_t c = sym(j);
+        if (j + kMtfAhead < 64) {
+            const uint32_t cn = sym(j + kMtfAhead);
+            plo[j + kMtfAhead] = s[a8(cn)];
+            pe[j + kMtfAhead] = lds_u32(s, ae(cn));
+        }
+        uint32_t t = plo[j] | (((pe[j] >> (c & 31u)) & 1u) << 8);
+#pragma unroll
+        for (int d = kMtfAhead; d >= 1; --d)  // updates the read-ahead missed, the nearest last
+            if (j >= d) t = c == sym(j - d) ? now + (uint32_t)(j - d) : t;
+        const uint32_t ab = (kRowBits << 8) + ((t >> 5) << 8) + l4;
+        const uint32_t ac = (kRowCnt << 8) + ((t >> 7) << 8) + l4;
+        const uint32_t bw = lds_u32(s, ab), cw = lds_u32(s, ac);
+        const uint32_t sw = (t >> 2) & 24u, ss = (t >> 4) & 24u;
+        const uint32_t rs = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << ss), 0u, 0u);
+        atomicXor((uint32_t *)(s + ab), 1u << (t & 31u));
+        atomicSub((uint32_t *)(s + ac), 1u << sw);
+        S -= 1u << ss;
+        // the new mark, slot now + j: word (now >> 5) + (j >> 5), counter byte of that word
+        atomicOr((uint32_t *)(s + bits0 + ((j >> 5) << 8)), 1u << (j & 31));
+        atomicAdd((uint32_t *)(s + cnt0), j < 32 ? inc0 : inc0 << 8);
+        S += sinc;
+        s[a8(c)] = (uint8_t)(now + (uint32_t)j);
+        atomicOr((uint32_t *)(s + ae(c)), 1u << (c & 31u));
+        __builtin_amdgcn_sched_barrier(0);
+        if (j > 0) {
+            uint32_t r = __builtin_amdgcn_sad_u8(pcw & (0xFFFFFF00u << psw), 0u,
+                                                 __builtin_popcount((pbw >> (pt & 31u)) >> 1) + pr);
+            asm volatile("" : "+v"(r));  // computed here, not sunk to the stores (64 symbols' terms live)
+            const int q = j - 1;
+            ow[q >> 2] = (q & 3) ? ow[q >> 2] | (r << (8 * (q & 3))) : r;
+        }
+        pbw = bw;
+        pcw = cw;
+        pt = t;
+        psw = sw;
+        pr = rs;
+    }
+    const uint32_t r = __builtin_amdgcn_sad_u8(pcw & (0xFFFFFF00u << psw), 0u,
+                                               __builtin_popcount((pbw >> (pt & 31u)) >> 1) + pr);
+    ow[15] |= r << 24;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o4[q] = make_uint4(ow[4 * q], ow[4 * q + 1], ow[4 * q + 2], ow[4 * q + 3]);
+}
+
 // Slots 0..255 marked (the start alphabet or the renumbered window), epochs cleared.
 __device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t &S)
 {
@@ -383,17 +461,7 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         load_sg(sg + 1, pf);
         if (whole(sg)) {
             uint4 o4[4];
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t iw[4] = {in[q].x, in[q].y, in[q].z, in[q].w};
-                uint32_t o[4] = {0, 0, 0, 0};
-#pragma unroll
-                for (uint32_t k = 0; k < 16; ++k) {
-                    const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
-                    o[k >> 2] |= mtf_step<false>(c, true, now + 16 * q, k, s, l4, S) << (8 * (k & 3));
-                }
-                o4[q] = make_uint4(o[0], o[1], o[2], o[3]);
-            }
+            mtf_whole(in, now, s, l4, S, o4);
             uint4 *po = (uint4 *)(out + a0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) po[q] = o4[q];

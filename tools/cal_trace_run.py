@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Encode Calgary files (default: pic) a few times for a rocprofv3 kernel trace; the last call is
+the one analysed by tools/round_trace.py. usage: python tools/cal_trace_run.py [file ...]"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "bwt-mtf-huffman-compressor_amd"))
+import bmh  # noqa: E402
+
+names = sys.argv[1:] or ["pic"]
+datas = [open(os.path.join(REPO, "tests", "golden", "calgary", f), "rb").read() for f in names]
+ctx = bmh.Context(0)
+arr = np.frombuffer(b"".join(datas), np.uint8)
+offs = np.cumsum([0] + [len(b) for b in datas]).astype(np.uint64)
+d_in = ctx.alloc(arr.size)
+d_in.upload(arr)
+cap = sum(int(bmh.lib().bmh_record_bound(len(b))) for b in datas)
+d_out = ctx.alloc(cap)
+for _ in range(3):
+    ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+ctx.sync()
+print("ok", names, arr.size)
