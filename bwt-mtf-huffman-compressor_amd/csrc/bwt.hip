@@ -2576,7 +2576,7 @@ void build_tiles(const std::vector<S> &segs, uint32_t tile, std::vector<T> &tile
 
 }  // namespace
 
-void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary)
+void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary)
 {
     const uint32_t nb = bt.nblocks;
     const uint64_t N = bt.total;

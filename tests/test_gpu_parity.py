@@ -584,22 +584,23 @@ def test_compress_host_multi_matches_single_context(ctx):
 
 
 def test_fresh_context_single_data_phase():
-    """a one-shot encode of Calgary's pic (a block that needs rank doubling)
-    on a fresh context runs the BWT data phase once — small batches store the full SA from the
-    start instead of re-running the data phase when doubling turns out to be needed — and its
-    record is still the reference's."""
+    """a one-shot encode of Calgary's progl (a block whose long repeats need
+    rank doubling) on a fresh context runs the BWT data phase once — small batches store the full
+    SA from the start instead of re-running the data phase when doubling turns out to be needed —
+    and its record is still the reference's. (pic, the first file this held for, now takes the
+    run-length path: tests/test_gpu_runs.py.)"""
     from oracle_ffi import GOLDEN
-    pic = open(os.path.join(GOLDEN, "calgary", "pic"), "rb").read()
-    gold = open(os.path.join(GOLDEN, "calgary_records", "pic.bzap"), "rb").read()
+    progl = open(os.path.join(GOLDEN, "calgary", "progl"), "rb").read()
+    gold = open(os.path.join(GOLDEN, "calgary_records", "progl.bzap"), "rb").read()
     with bmh.Context(0) as fresh:
         fresh.reset_stats()
         fresh.set_timing(True)
-        rec = fresh.encode_blocks([pic])[0]
+        rec = fresh.encode_blocks([progl])[0]
         st = fresh.kernel_stats()
         fresh.set_timing(False)
     assert rec == gold
     assert st["bwt_g1_scatter"][0] == 1, st.get("bwt_g1_scatter")
-    assert st.get("bwt_rank_fill", (0, 0))[0] == 1  # pic does need the doubling phase
+    assert st.get("bwt_rank_fill", (0, 0))[0] == 1  # progl does need the doubling phase
 
 
 def test_compress_host_multi_distinct_devices(ctx):

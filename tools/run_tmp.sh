@@ -1,8 +1,8 @@
 export TMPDIR=/tmp
-BMH_LIB=variants/v2/libbmh.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "bwt or manifest or calgary or fuzz or large" > gpurun_out/v2_tests.log 2>&1; tail -2 gpurun_out/v2_tests.log
-for v in pv1 pv2; do
-BMH_LIB=variants/$v/libbmh.so timeout -k 10 120 python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 > gpurun_out/$v.json 2> gpurun_out/$v.err
-echo $v; grep phases gpurun_out/$v.err | tail -1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_runs.py -x -v --timeout 120 --timeout-method thread > gpurun_out/runs_tests.log 2>&1; rc=$?; tail -25 gpurun_out/runs_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "calgary or fresh or manifest or fuzz" > gpurun_out/runs_tests2.log 2>&1; rc=$?; tail -3 gpurun_out/runs_tests2.log; [ $rc -eq 0 ] || exit $rc
+ALL="bib book1 book2 geo news obj1 obj2 paper1 paper2 pic progc progl progp trans"
+for s in 2 3; do
+  BMH_STREAMS=$s timeout -k 10 60 python3 tools/cal_subset_time.py $ALL || exit 1
 done
-bash tools/variant_bench.sh v2
-bash tools/run_pmc.sh v2
+timeout -k 10 60 python3 tools/cal_subset_time.py pic || exit 1
