@@ -228,12 +228,17 @@ static Ctx *sub_ctx(Ctx *c, size_t i)
     return x;
 }
 
-static int stream_count(Ctx *c)
+// Default sub-pipelines: 3 for batches under 128 MiB (their list rounds leave the GPU idle
+// between host waits, so a third pipeline fills it: Calgary 5.9 -> 5.1 ms, Zipf 100 MB at 1 MiB
+// blocks 11.8 -> 11.1-11.4 ms), 2 above (the 128 MiB text batch, the 256 MiB streamed batches
+// and the 1 GiB headline measured equal or slower with 3; 4+ exceed the device's 4 hardware
+// queues and serialise: Calgary 7.9 ms).
+static int stream_count(Ctx *c, uint64_t total)
 {
     if (c->nstreams > 0) return c->nstreams;
     const char *e = getenv("BMH_STREAMS");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? std::min(v, 16) : 2;
+    return v > 0 ? std::min(v, 16) : total < (128ull << 20) ? 3 : 2;
 }
 
 // The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
@@ -244,7 +249,7 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
                    uint64_t *rec_offs)
 {
     const uint32_t nb = bt.nblocks;
-    const int S = (int)std::min<uint32_t>((uint32_t)stream_count(c), nb / 2);
+    const int S = (int)std::min<uint32_t>((uint32_t)stream_count(c, bt.total), nb / 2);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
         return;

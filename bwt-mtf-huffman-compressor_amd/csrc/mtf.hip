@@ -550,48 +550,53 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
 // First occurrence of each MTF value per block (huffman() main.cpp:238-244 orders the leaves
 // by it). The pack-chunk histograms say in which chunk each value first appears (value v:
 // the first chunk with a nonzero count, found 16 chunks per step); only those chunks are
-// scanned, once per distinct first chunk (on random data: the block's first chunk alone).
-__global__ __launch_bounds__(256) void k_mtf_first(const uint8_t *__restrict__ in, const uint32_t *__restrict__ boffs,
-                                                   const uint32_t *__restrict__ pfirst, const uint32_t *__restrict__ freq,
-                                                   const uint16_t *__restrict__ chist, uint32_t *__restrict__ first)
+// scanned (on random data: the block's first chunk alone), one wave per distinct chunk. A value
+// has one first chunk, so the chunks are independent and need no order (a block whose values
+// first appear in 256 different chunks — Calgary pic — scans them 16 at a time).
+constexpr uint32_t kFirstNT = 1024;
+__global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restrict__ in, const uint32_t *__restrict__ boffs,
+                                                        const uint32_t *__restrict__ pfirst,
+                                                        const uint32_t *__restrict__ freq,
+                                                        const uint16_t *__restrict__ chist, uint32_t *__restrict__ first)
 {
-    __shared__ uint32_t f[256], s_cv[256], s_min[5];
-    const uint32_t b = blockIdx.x, v = threadIdx.x;
+    __shared__ uint32_t f[256], s_cv[256], s_list[256], s_nlist;
+    const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63u;
     const uint32_t c0 = pfirst[b], nc = pfirst[b + 1] - c0;
     const uint32_t o = boffs[b], n = boffs[b + 1] - o;
-    f[v] = 0xffffffffu;
-    uint32_t cv = 0xffffffffu;  // first chunk holding v (block-relative); none for absent values
-    bool look = freq[(size_t)b * 256 + v] != 0;
-    for (uint32_t base = 0; __syncthreads_or(look && base < nc); base += 16) {
-        if (!look) continue;
-        uint32_t cnt[16];
+    if (t == 0) s_nlist = 0;
+    if (t < 256) {
+        f[t] = 0xffffffffu;
+        uint32_t cv = 0xffffffffu;  // first chunk holding t (block-relative); none for absent values
+        bool look = freq[(size_t)b * 256 + t] != 0;
+        for (uint32_t base = 0; look && base < nc; base += 16) {
+            uint32_t cnt[16];
 #pragma unroll
-        for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + v] : 0u;
+            for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + t] : 0u;
 #pragma unroll
-        for (int j = 15; j >= 0; --j)
-            if (cnt[j]) cv = base + j;
-        look = cv == 0xffffffffu;
+            for (int j = 15; j >= 0; --j)
+                if (cnt[j]) cv = base + j;
+            look = cv == 0xffffffffu;
+        }
+        s_cv[t] = cv;
     }
-    s_cv[v] = cv;
-    uint32_t todo = cv;
-    for (;;) {  // the distinct first chunks, smallest first
-        uint32_t m = todo;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, off, 64));
-        if ((v & 63u) == 0) s_min[v >> 6] = m;
-        __syncthreads();
-        const uint32_t cm = min(min(s_min[0], s_min[1]), min(s_min[2], s_min[3]));
-        __syncthreads();
-        if (cm == 0xffffffffu) break;
-        const uint32_t p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
-        for (uint32_t i = v; i < len; i += 256) {
+    __syncthreads();
+    if (t < 256) {  // the smallest value of each distinct first chunk lists it
+        const uint32_t cv = s_cv[t];
+        bool lead = cv != 0xffffffffu;
+        for (uint32_t u = 0; u < t && lead; ++u) lead = s_cv[u] != cv;
+        if (lead) s_list[atomicAdd(&s_nlist, 1u)] = cv;
+    }
+    __syncthreads();
+    const uint32_t nl = s_nlist;
+    for (uint32_t k = w; k < nl; k += kFirstNT / 64) {
+        const uint32_t cm = s_list[k], p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
+        for (uint32_t i = l; i < len; i += 64) {
             const uint32_t x = in[o + p0 + i];
             if (s_cv[x] == cm) atomicMin(&f[x], p0 + i);
         }
-        if (todo == cm) todo = 0xffffffffu;
     }
     __syncthreads();
-    first[(size_t)b * 256 + v] = f[v];
+    if (t < 256) first[(size_t)b * 256 + t] = f[t];
 }
 
 }  // namespace
@@ -711,7 +716,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist);
-    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, 256, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist, d_first);
+    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist, d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     if (h_freq32 || h_first32) c->sync();
