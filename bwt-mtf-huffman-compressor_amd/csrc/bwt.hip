@@ -2020,6 +2020,10 @@ __device__ __forceinline__ void group_fill_elem(const DataArgs &a, const Seg4 &s
     if (s.w & kFinalFlag) put_final(a, b, boff, n, a.data + boff, s.x + e, p, s.x - boff);
 }
 
+// Groups of up to kLaneGroup members are filled one per lane (a text's data phase leaves
+// ~100 K groups of 2-3 rotations; a wave per group idled 62 lanes and appended with one atomic
+// per group); longer ones take the whole wave, one at a time. One atomicMin per wave.
+constexpr uint32_t kLaneGroup = 16;
 __global__ __launch_bounds__(256) void k_group_fill(DataArgs a, const Seg4 *__restrict__ groups, uint32_t ng,
                                                     uint32_t *__restrict__ rkA, uint32_t *__restrict__ rkB,
                                                     uint2 *__restrict__ segs, uint32_t *__restrict__ coop, Counters *cnt)
@@ -2027,18 +2031,36 @@ __global__ __launch_bounds__(256) void k_group_fill(DataArgs a, const Seg4 *__re
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
     const uint32_t l = threadIdx.x & 63u;
-    for (uint32_t g = wave; g < ng; g += nwaves) {
-        const Seg4 s = groups[g];
-        if (s.y > kCoopGroup) {
-            if (l == 0) coop[atomicAdd(&cnt->coop_fill, 1u)] = g;
-            continue;
+    uint32_t dmin = 0xffffffffu;
+    for (uint32_t base = wave * 64u; base < ng; base += nwaves * 64u) {
+        const uint32_t g = base + l;
+        const Seg4 s = g < ng ? groups[g] : Seg4{0, 0, 0, 0};
+        if (g < ng && s.y <= kLaneGroup) {
+            for (uint32_t e = 0; e < s.y; ++e) group_fill_elem(a, s, e, rkA, rkB);
+            if (!(s.w & kFinalFlag)) {
+                segs[wave_append(&cnt->next)] = make_uint2(s.x, s.y);
+                dmin = min(dmin, s.z);
+            }
         }
-        for (uint32_t e = l; e < s.y; e += 64) group_fill_elem(a, s, e, rkA, rkB);
-        if (!(s.w & kFinalFlag) && l == 0) {
-            segs[wave_append(&cnt->next)] = make_uint2(s.x, s.y);
-            atomicMin(&cnt->dmin_bits, s.z);
+        uint64_t big = __ballot(g < ng && s.y > kLaneGroup);
+        while (big) {
+            const uint32_t j = (uint32_t)__builtin_ctzll(big);
+            big &= big - 1;
+            const Seg4 t = groups[base + j];
+            if (t.y > kCoopGroup) {
+                if (l == 0) coop[atomicAdd(&cnt->coop_fill, 1u)] = base + j;
+                continue;
+            }
+            for (uint32_t e = l; e < t.y; e += 64) group_fill_elem(a, t, e, rkA, rkB);
+            if (!(t.w & kFinalFlag) && l == 0) {
+                segs[atomicAdd(&cnt->next, 1u)] = make_uint2(t.x, t.y);
+                dmin = min(dmin, t.z);
+            }
         }
     }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, off, 64));
+    if (l == 0 && dmin != 0xffffffffu) atomicMin(&cnt->dmin_bits, dmin);
 }
 
 __global__ __launch_bounds__(256) void k_group_fill_coop(DataArgs a, const Seg4 *__restrict__ groups,
@@ -2935,7 +2957,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         BMH_HIP(hipMemsetAsync(&d_cnt->dmin_bits, 0xff, 4, c->stream));
         uint32_t *coop = (uint32_t *)c->get(WS_COOP, (size_t)ngroups * 4 + (N / kCoopGroup + 2) * 4 + 64);
         BMH_HIP(hipMemsetAsync(&d_cnt->coop_fill, 0, 4, c->stream));
-        BMH_LAUNCH(c, "bwt_group_fill", k_group_fill, std::min<uint32_t>(cdiv(ngroups, 4), 65536), 256, 0, da, dgroups,
+        BMH_LAUNCH(c, "bwt_group_fill", k_group_fill, std::min<uint32_t>(cdiv(ngroups, 256), 65536), 256, 0, da, dgroups,
                    ngroups, rkA, rkB, seg_cur, coop, d_cnt);
         BMH_LAUNCH(c, "bwt_group_fill", k_group_fill_coop, kCoopGrid, 256, 0, da, dgroups, coop, rkA, rkB, seg_cur, d_cnt);
         read_counters();
