@@ -70,16 +70,27 @@ __global__ __launch_bounds__(256) void k_run_count(const uint8_t *__restrict__ i
     if ((threadIdx.x & 63u) == 0 && k) atomicAdd(&count[b], k);
 }
 
-// Gather / scatter whole blocks between two layouts: grid (tiles of 64 KiB, blocks).
+// Gather / scatter whole blocks between two layouts: grid (tiles of kMoveTile bytes, blocks),
+// 16 bytes a thread (byte loads; the offsets carry no alignment).
+constexpr uint32_t kMoveTile = 4096;
 __global__ __launch_bounds__(256) void k_move_blocks(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
                                                      const uint64_t *__restrict__ so, const uint64_t *__restrict__ dofs,
                                                      const uint64_t *__restrict__ len)
 {
     const uint32_t b = blockIdx.y;
     const uint64_t n = len[b], s0 = so[b], d0 = dofs[b];
-    for (uint64_t i = (uint64_t)blockIdx.x * 65536u + threadIdx.x; i < n && i < (uint64_t)(blockIdx.x + 1) * 65536u;
-         i += 256)
-        dst[d0 + i] = src[s0 + i];
+    const uint64_t i0 = (uint64_t)blockIdx.x * kMoveTile + threadIdx.x;
+    uint8_t v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = i0 + 256u * k;
+        v[k] = i < n ? src[s0 + i] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = i0 + 256u * k;
+        if (i < n) dst[d0 + i] = v[k];
+    }
 }
 
 __global__ __launch_bounds__(256) void k_prim_scatter(const uint32_t *__restrict__ tmp, const uint32_t *__restrict__ map,
@@ -368,7 +379,7 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         } else {
             uint8_t *tin = (uint8_t *)c->get(WS_RUN_IN, sb.total);
             uint8_t *tL = (uint8_t *)c->get(WS_RUN_L, sb.total);
-            const dim3 grid(cdiv(sb.max_n, 65536), nk);
+            const dim3 grid(cdiv(sb.max_n, kMoveTile), nk);
             BMH_LAUNCH(c, "bwt_run_move", k_move_blocks, grid, 256, 0, d_in, tin, d_so, d_co, d_len);
             bwt_batch_core(c, tin, sb, tL, nullptr);
             BMH_LAUNCH(c, "bwt_run_move", k_move_blocks, grid, 256, 0, tL, d_L, d_co, d_so, d_len);

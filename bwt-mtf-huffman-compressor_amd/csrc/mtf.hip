@@ -588,11 +588,36 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
     }
     __syncthreads();
     const uint32_t nl = s_nlist;
-    for (uint32_t k = w; k < nl; k += kFirstNT / 64) {
+    for (uint32_t k = w; k < nl; k += kFirstNT / 64) {  // lane l: symbols [64l, 64l + 64) of the chunk
         const uint32_t cm = s_list[k], p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
-        for (uint32_t i = l; i < len; i += 64) {
-            const uint32_t x = in[o + p0 + i];
-            if (s_cv[x] == cm) atomicMin(&f[x], p0 + i);
+        const uint32_t e0 = 64 * l;
+        uint32_t sw[16];
+        if (e0 + 64 <= len && ((o + p0 + e0) & 15u) == 0) {
+            const uint4 *p = (const uint4 *)(in + o + p0 + e0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = p[q];
+                sw[4 * q] = v.x;
+                sw[4 * q + 1] = v.y;
+                sw[4 * q + 2] = v.z;
+                sw[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                uint32_t wv = 0;
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t i = e0 + 4 * q + j;
+                    wv |= (i < len ? (uint32_t)in[o + p0 + i] : 0u) << (8 * j);
+                }
+                sw[q] = wv;
+            }
+        }
+        const uint32_t m = e0 < len ? min(64u, len - e0) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t x = (sw[j >> 2] >> (8 * (j & 3))) & 255u;
+            if (j < m && s_cv[x] == cm) atomicMin(&f[x], p0 + e0 + j);
         }
     }
     __syncthreads();
