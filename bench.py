@@ -412,9 +412,6 @@ def main() -> None:
                "roundtrip_bit_exact": bool(ok)}
         d_dec.free()
 
-    # Calgary before the host-buffer leg: its third sub-pipeline stream is created on first use,
-    # and created after the host-buffer copy streams it shares a hardware queue with another
-    # pipeline (the device has 4): 4.4 -> 7.3 ms
     cal = calgary_leg(ctx, a.calgary_steps) if (a.calgary_steps > 0 and r.rank == 0) else None
     pcie = pcie_leg(r, enc, a.pcie_steps, 1) if a.pcie_steps > 0 else None
 

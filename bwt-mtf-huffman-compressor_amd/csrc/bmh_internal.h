@@ -59,6 +59,7 @@ struct Ctx {
     int device = 0;
     int cus = 256;  // compute units of the device (persistent-grid sizing)
     hipStream_t stream = nullptr;
+    bool own_stream = true;  // sub-pipelines 0 and 2 borrow the context / H2D stream (capi.cpp)
     bool timing = false;
     std::map<std::string, KStat> stats;
     struct Pending {

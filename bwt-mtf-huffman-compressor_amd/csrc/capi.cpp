@@ -211,18 +211,46 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
     if (st & kStatusPrimary) fail(BMH_EHIP, "bwt: internal error (primary index not produced)");
 }
 
+// Streams and hardware queues: the device exposes 4 hardware queues per process
+// (GPU_MAX_HW_QUEUES); HIP gives each of the first 4 streams its own and makes later ones share
+// the least-used queue, and a stream that shares a queue serialises with the other's work. So a
+// context creates exactly 4 streams, once, and gives them roles that are never busy together:
+//   A = the context stream = pipeline 0        C = pipeline 2 = the H2D copy stream
+//   B = pipeline 1                             D = the D2H copy stream
+// Device-resident batches run up to 3 pipelines (A, B, C); the host-buffer path runs 2 (A, B)
+// next to its copies (C, D). Streams made on demand instead put a third pipeline on pipeline
+// 0's queue when the copy streams came first (Calgary 4.4 -> 7.3 ms), or the D2H copies behind a
+// pipeline when it came first (PCIe-inclusive 30 -> 47-59 ms per GiB); per-call streams paid a
+// queue set-up each call (Calgary 8.5 ms). Pipelines past 3 (BMH_STREAMS) get streams of their
+// own and share queues.
+static Ctx *new_sub(Ctx *c, hipStream_t borrowed)
+{
+    Ctx *x = new bmh_ctx();
+    x->device = c->device;
+    x->cus = c->cus;
+    if (borrowed) {
+        x->stream = borrowed;
+        x->own_stream = false;
+    } else if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete x;
+        fail(BMH_EHIP, "stream creation failed");
+    }
+    c->subs.push_back(x);
+    return x;
+}
+
+static void create_streams(Ctx *c)
+{
+    new_sub(c, c->stream);  // pipeline 0 on A
+    new_sub(c, nullptr);    // pipeline 1: B
+    BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));  // C
+    new_sub(c, c->s_h2d);   // pipeline 2 on C
+    BMH_HIP(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));  // D
+}
+
 static Ctx *sub_ctx(Ctx *c, size_t i)
 {
-    while (c->subs.size() <= i) {
-        Ctx *x = new bmh_ctx();
-        x->device = c->device;
-        x->cus = c->cus;
-        if (hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
-            delete x;
-            fail(BMH_EHIP, "stream creation failed");
-        }
-        c->subs.push_back(x);
-    }
+    while (c->subs.size() <= i) new_sub(c, nullptr);
     Ctx *x = c->subs[i];
     x->timing = c->timing;
     return x;
@@ -246,10 +274,11 @@ static int stream_count(Ctx *c, uint64_t total)
 // LDS-bound ones. Records land back to back in block order: each run's offset scan starts
 // from the previous run's end (OffsetChain).
 void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
-                   uint64_t *rec_offs)
+                   uint64_t *rec_offs, int max_pipes)
 {
     const uint32_t nb = bt.nblocks;
-    const int S = (int)std::min<uint32_t>((uint32_t)stream_count(c, bt.total), nb / 2);
+    const int S = (int)std::min<uint32_t>(std::min<uint32_t>((uint32_t)stream_count(c, bt.total), (uint32_t)max_pipes),
+                                          nb / 2);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
         return;
@@ -393,8 +422,6 @@ static bool is_pinned(const void *p, uint64_t bytes, int dev)
 // and is released with the context.
 static void ensure_staging(Ctx *c, size_t in_bytes, size_t out_bytes, int ns)
 {
-    if (!c->s_h2d) BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));
-    if (!c->s_d2h) BMH_HIP(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));
     auto grow = [](uint8_t *&p, size_t &have, size_t need) {
         if (need == 0 || have >= need) return;
         if (p) BMH_HIP(hipHostFree(p));
@@ -569,7 +596,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
             const B &bt = batches[k];
             Batch b = make_batch(bt.offs.data(), (uint32_t)bt.blocks.size());
             ro[k].resize(bt.blocks.size() + 1);
-            encode_blocks(c, d_in[s], b, d_out[s], bt.cap, ro[k].data());
+            encode_blocks(c, d_in[s], b, d_out[s], bt.cap, ro[k].data(), 2);  // pipelines A, B (create_streams)
             bump(encoded);
             if (!wait_for([&] { return written + NS > k; })) return;  // the writer is done with stage_out[s]
             const uint64_t bytes = ro[k][bt.blocks.size()];
@@ -737,6 +764,12 @@ bmh_status bmh_ctx_create(int device, bmh_ctx **out)
         delete c;
         fail(BMH_EHIP, "stream creation failed");
     }
+    try {
+        create_streams(c);
+    } catch (...) {
+        bmh_ctx_destroy(c);
+        throw;
+    }
     *out = c;
     API_END
 }
@@ -763,7 +796,7 @@ void bmh_ctx_destroy(bmh_ctx *c)
         (void)hipEventDestroy(p.b);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    (void)hipStreamDestroy(c->stream);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -904,7 +937,7 @@ bmh_status bmh_encode_blocks_dev(bmh_ctx *c, const uint8_t *d_in, const uint64_t
     use_device(c);
     if (!d_in || !d_out || !h_rec_offs) fail(BMH_EINVAL, "null argument");
     Batch bt = make_batch(offs, nblocks);
-    encode_blocks(c, d_in, bt, d_out, out_cap, h_rec_offs);
+    encode_blocks(c, d_in, bt, d_out, out_cap, h_rec_offs, 16);
     API_END
 }
 
