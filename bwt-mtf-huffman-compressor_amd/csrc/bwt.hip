@@ -94,6 +94,11 @@ constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries pe
 constexpr uint32_t kTinyQ = BMH_TINY_Q;        // the packed tiny finish (256 segments per workgroup)
 // doubling phase
 constexpr uint32_t kTinyMax = 64;     // doubling-phase segments ranked by wave shuffles (k_dtiny)
+#ifndef BMH_TINY_EPW
+#define BMH_TINY_EPW 16
+#endif
+constexpr uint32_t kTinyEpwShort = BMH_TINY_EPW;  // tiny-list entries per wave for short lists
+constexpr uint32_t kTinyWideList = 1u << 17;      // lists this long keep 64 entries per wave
 constexpr uint32_t kDblGrid = 1024;   // fixed grid of the doubling-phase kernels (counts read on the device)
 constexpr uint32_t kMedMax = 4096;
 constexpr uint32_t kFinalFlag = 0x80000000u;
@@ -1098,24 +1103,26 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 // splits across rounds); each rotation is ranked inside its segment by the next 64 rotation
 // bits with wave shuffles. Tie groups of 2-5 rotations are the common case on text, so a wave
 // per segment would leave most lanes idle.
+// epw = list entries per wave (64, or 16 / 32 when a round's tiny list is short: a wave walks
+// its entries' rotations in rounds of 64, so short lists finish sooner spread over more waves)
 __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ lists,
                                                      const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
-                                                     LaneMap lm)
+                                                     LaneMap lm, uint32_t epw)
 {
     __shared__ DeferQueue<kTinyQ> dq;
-    // workgroup i: sub-list x of its XCD lane, entries [256 j, + 256)
+    // workgroup i: sub-list x of its XCD lane, entries [4 epw j, + 4 epw)
     uint32_t x, j, step;
     lane_of(lm, blockIdx.x, x, j, step, gridDim.x >> 3);
     const uint32_t nlist = cnt[x];
     const Seg4 *__restrict__ list = lists + loff[x];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
     {
-        const uint32_t g0 = j * 256;
+        const uint32_t g0 = j * 4 * epw;
         dq_init(dq);
         __syncthreads();
-        const uint32_t i0 = g0 + w * 64;
+        const uint32_t i0 = g0 + w * epw;
         if (i0 < nlist) {  // wave-uniform
-            const Seg4 sgl = i0 + l < nlist ? list[i0 + l] : make_uint4(0, 0, 0, 0);
+            const Seg4 sgl = l < epw && i0 + l < nlist ? list[i0 + l] : make_uint4(0, 0, 0, 0);
             const uint32_t incl = wave_incl_sum(sgl.y), st = incl - sgl.y;
             const uint32_t total = __shfl(incl, 63, 64);
             for (uint32_t base = 0; base < total;) {  // wave-uniform rounds
@@ -2853,9 +2860,11 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             BMH_HIP(hipMemsetAsync(&d_cnt->lc[out][0][0], 0, sizeof(d_cnt->lc[out]), c->stream));
             set_out(out);
             const uint32_t *dc = &d_cnt->lc[in][0][0];
-            if (tot[kListTiny])
-                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 256), 256, 0, da, lt[in],
-                           d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny]);
+            if (tot[kListTiny]) {
+                const uint32_t epw = tot[kListTiny] >= kTinyWideList ? 64u : kTinyEpwShort;
+                BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * cdiv(rows[kListTiny], 4 * epw), 256, 0, da, lt[in],
+                           d_loff + kListTiny * 9, dc + kListTiny * 8, lm[kListTiny], epw);
+            }
             if (tot[kListFin]) {
                 // size classes: <= 128 and <= 512 one wave each (4 segments per workgroup), then 2, 4
                 // and 8 waves of 8 elements a thread (every wave of a class holds slots of its
