@@ -52,7 +52,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_IN3, WS_OUT3, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_COUNT_
 };
 
 struct Ctx {
@@ -90,6 +90,10 @@ struct Ctx {
 
     // sub-pipelines (own stream + workspaces) a batch is split across (capi.cpp)
     std::vector<Ctx *> subs;
+    // side context on the context's D2H stream (idle outside host-buffer calls): the run-length
+    // BWT of a batch's run-heavy blocks runs there beside the rotation sorter (bwt_runs.hip)
+    hipStream_t aux_stream = nullptr;
+    Ctx *aux = nullptr;
     int nstreams = 0;  // 0: BMH_STREAMS or the default
     // BWT: write the suffix array of every slot (needed by rank doubling) instead of only the
     // slots later passes read; set after a batch needed doubling, cleared when one did not
@@ -190,6 +194,7 @@ constexpr uint32_t kStatusEmpty = 1, kStatusCodeLen = 2, kStatusPrimary = 4, kSt
 // Stage implementations (device buffers). bwt_batch / mtf_batch synchronise only when they
 // return host outputs (h_primary / h_freq32 non-null).
 void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);  // bwt_runs.hip
+Ctx *aux_ctx(Ctx *c);  // capi.cpp
 // the rotation sorter alone (bwt.hip); bwt_batch routes run-heavy blocks of small batches around it
 void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,

@@ -31,6 +31,8 @@
 #include "bmh_internal.h"
 
 #include <algorithm>
+#include <exception>
+#include <thread>
 #include <rocprim/rocprim.hpp>
 
 #include "device_util.h"
@@ -325,9 +327,10 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         return;
     }
     // ---- screen: cyclic run count of every block
-    uint8_t *d_misc = (uint8_t *)c->get(WS_RUN_MISC, (size_t)(nb + 1) * 8 + (size_t)nb * 4 + 1024);
+    uint8_t *d_misc = (uint8_t *)c->get(WS_RUN_MISC, (size_t)(nb + 1) * 8 + (size_t)nb * 8 + 1024);
     uint64_t *d_boffs = (uint64_t *)d_misc;
     uint32_t *d_count = (uint32_t *)(d_misc + (size_t)(nb + 1) * 8);
+    uint32_t *d_rmap = d_count + nb;  // run-path block indices
     std::vector<uint32_t> runs(nb);
     c->h2d(d_boffs, bt.offs.data(), (size_t)(nb + 1) * 8);
     BMH_HIP(hipMemsetAsync(d_count, 0, (size_t)nb * 4, c->stream));
@@ -345,7 +348,19 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         return;
     }
     uint32_t *d_prim = (uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);  // full-batch capacity first
-    if (!keep.empty()) {
+    // the run blocks' primaries go to a side array of the context that runs them, then to d_prim
+    uint32_t *rp = nullptr;
+    auto run_blocks = [&](Ctx *x) {
+        WallPhase wall(x, "bwt_runs");
+        uint32_t *p = (uint32_t *)x->get(WS_RUN_PRIM, rb.size() * 4 + 64);
+        uint32_t h_cnt = 0;
+        for (size_t i = 0; i < rb.size(); ++i) {
+            const uint64_t o = bt.offs[rb[i]];
+            run_block(x, d_in + o, (uint32_t)(bt.offs[rb[i] + 1] - o), runs[rb[i]], d_L + o, p + i, &h_cnt);
+        }
+        rp = p;
+    };
+    auto sorter_blocks = [&]() {
         // the sorter blocks as one contiguous batch (in place when they already are one); its
         // primaries land in WS_PRIMARY[0 .. keep) and are moved to their blocks' slots
         const uint32_t nk = (uint32_t)keep.size();
@@ -388,13 +403,41 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
             BMH_HIP(hipMemcpyAsync(d_tprim, d_prim, (size_t)nk * 4, hipMemcpyDeviceToDevice, c->stream));
             BMH_LAUNCH(c, "bwt_run_move", k_prim_scatter, cdiv(nk, 256), 256, 0, d_tprim, d_map, nk, d_prim);
         }
+    };
+    if (keep.empty()) {
+        run_blocks(c);
+    } else {
+        // the run path on the side context (its own stream and workspaces, one host thread)
+        // beside the rotation sorter: they write disjoint L ranges and primary arrays
+        Ctx *x = aux_ctx(c);
+        std::exception_ptr err;
+        std::thread th([&] {
+            try {
+                BMH_HIP(hipSetDevice(c->device));
+                run_blocks(x);
+                x->sync();
+            } catch (...) {
+                err = std::current_exception();
+            }
+        });
+        try {
+            sorter_blocks();
+        } catch (...) {
+            th.join();
+            throw;
+        }
+        th.join();
+        if (err) std::rethrow_exception(err);
+        if (c->timing) {
+            for (auto &kv : x->stats) {
+                c->stats[kv.first].launches += kv.second.launches;
+                c->stats[kv.first].ms += kv.second.ms;
+            }
+            x->stats.clear();
+        }
     }
-    WallPhase wall(c, "bwt_runs");
-    uint32_t h_cnt = 0;
-    for (uint32_t b : rb) {
-        const uint64_t o = bt.offs[b];
-        run_block(c, d_in + o, (uint32_t)(bt.offs[b + 1] - o), runs[b], d_L + o, d_prim + b, &h_cnt);
-    }
+    c->h2d(d_rmap, rb.data(), rb.size() * 4);
+    BMH_LAUNCH(c, "bwt_run_move", k_prim_scatter, cdiv(rb.size(), 256), 256, 0, rp, d_rmap, (uint32_t)rb.size(), d_prim);
     if (h_primary) {
         std::vector<uint32_t> hp(nb);
         c->d2h(hp.data(), d_prim, (size_t)nb * 4);

@@ -246,11 +246,27 @@ static void create_streams(Ctx *c)
     BMH_HIP(hipStreamCreateWithFlags(&c->s_h2d, hipStreamNonBlocking));  // C
     new_sub(c, c->s_h2d);   // pipeline 2 on C
     BMH_HIP(hipStreamCreateWithFlags(&c->s_d2h, hipStreamNonBlocking));  // D
+    c->aux_stream = c->s_d2h;
+    for (Ctx *x : c->subs) x->aux_stream = c->s_d2h;
+}
+
+Ctx *aux_ctx(Ctx *c)
+{
+    if (!c->aux) {
+        Ctx *x = new bmh_ctx();
+        x->device = c->device;
+        x->cus = c->cus;
+        x->stream = c->aux_stream ? c->aux_stream : c->stream;
+        x->own_stream = false;
+        c->aux = x;
+    }
+    c->aux->timing = c->timing;
+    return c->aux;
 }
 
 static Ctx *sub_ctx(Ctx *c, size_t i)
 {
-    while (c->subs.size() <= i) new_sub(c, nullptr);
+    while (c->subs.size() <= i) new_sub(c, nullptr)->aux_stream = c->s_d2h;
     Ctx *x = c->subs[i];
     x->timing = c->timing;
     return x;
@@ -779,6 +795,8 @@ void bmh_ctx_destroy(bmh_ctx *c)
     if (!c) return;
     for (auto *x : c->subs) bmh_ctx_destroy(static_cast<bmh_ctx *>(x));
     c->subs.clear();
+    if (c->aux) bmh_ctx_destroy(static_cast<bmh_ctx *>(c->aux));
+    c->aux = nullptr;
     if (c->arena) (void)hipHostFree(c->arena);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
