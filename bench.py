@@ -11,7 +11,9 @@ HBM.
   --scaling strong 1 GiB in total (256 blocks) dealt over the N GPUs (config 4 as written).
 value = input bytes of all ranks x steps / max-over-ranks time.
 
-Beside `value` (device-resident, the contract's figure) the line carries:
+`value` is the device-resident rate (inputs already in HBM, records left in HBM) that the
+driver's bench contract asks for. It is NOT SURVEY §8(d)'s graded figure: that is
+`pcie_inclusive` below, the number README quotes first. The line carries:
   pcie_inclusive  SURVEY §8(d)'s graded t_encode: the same blocks streamed by bmh_compress_host
                   from page-locked host memory (first H2D) to the records in page-locked host
                   memory (last D2H), and its graded roofline fraction.
