@@ -70,6 +70,8 @@ _SIGS = {
     "bmh_mtf_dev": (C.c_int, [P, P, PU64, U32, P, PU64, PU64]),
     "bmh_histogram_dev": (C.c_int, [P, P, PU64, U32, PU64, PU64]),
     "bmh_huffman_build": (C.c_int, [PU64, PU64, C.POINTER(CodeTable)]),
+    "bmh_huffman_build_sized": (C.c_int, [PU64, PU64, U64, C.POINTER(CodeTable)]),
+    "bmh_node_ranks": (C.c_int, [U64, U32, C.POINTER(C.c_uint16)]),
     "bmh_payload_bytes": (U64, [C.POINTER(CodeTable), PU64]),
     "bmh_pack_dev": (C.c_int, [P, P, PU64, U32, C.POINTER(CodeTable), P, PU64]),
     "bmh_encode_blocks_dev": (C.c_int, [P, P, PU64, U32, P, U64, PU64]),
@@ -368,12 +370,25 @@ def record_to_mtf(rec) -> bytes:
     return out[: n.value].tobytes()
 
 
-def huffman_build(freq: np.ndarray, first: np.ndarray) -> CodeTable:
+def huffman_build(freq: np.ndarray, first: np.ndarray, n: int = 0) -> CodeTable:
+    """The tree of huffman() (main.cpp:245-254) for a block of n bytes (n = 0: size unknown,
+    the closed-form tie-break of SURVEY App. B.3; below 128 KiB the order of the reference's
+    heap history for that size, include/bmh.h bmh_huffman_build_sized)."""
     f = np.ascontiguousarray(freq, dtype=np.uint64)
     fi = np.ascontiguousarray(first, dtype=np.uint64)
     t = CodeTable()
-    _check(lib().bmh_huffman_build(_u64p(f), _u64p(fi), C.byref(t)), "huffman_build")
+    _check(lib().bmh_huffman_build_sized(_u64p(f), _u64p(fi), n, C.byref(t)), "huffman_build")
     return t
+
+
+def node_ranks(n: int, L: int) -> tuple[list[int], bool]:
+    """Address ranks of the 2L - 1 tree nodes of an n-byte block, and whether they come from the
+    reference's heap history (True) or the closed form (False)."""
+    buf = (C.c_uint16 * 511)()
+    r = lib().bmh_node_ranks(n, L, buf)
+    if r < 0:
+        raise BmhError(BMH_EINVAL, "node_ranks: L must be 1..256")
+    return list(buf[: 2 * L - 1]), r == 1
 
 
 def payload_bytes(table: CodeTable, freq: np.ndarray) -> int:
@@ -455,7 +470,7 @@ def huffman(mtf, ctx: Context | None = None) -> tuple[bytes, CodeTable]:
         d_m.upload(a)
         freq, first = ctx.histogram_dev(d_m, offs)
         freq, first = freq[0], first[0]
-        t = huffman_build(freq, first)
+        t = huffman_build(freq, first, a.size)  # the MTF stream has the block's size
         nbytes = payload_bytes(t, freq)
         d_out = ctx.alloc(nbytes + 8)
         try:
@@ -514,5 +529,5 @@ def decompress(encoded_file_name: str, decoded_file_name: str) -> None:
 
 __all__ = ["BmhError", "CodeTable", "Context", "DevBuf", "lib", "bwt", "move_to_front", "huffman",
            "tree_to_bytes", "compress", "decompress", "compress_bytes_multi", "decompress_bytes",
-           "record_to_mtf", "huffman_build", "payload_bytes", "container_records", "is_container",
+           "record_to_mtf", "huffman_build", "node_ranks", "payload_bytes", "container_records", "is_container",
            "metrics_line", "default_context"]

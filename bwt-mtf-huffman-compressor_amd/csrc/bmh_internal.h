@@ -52,7 +52,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_IN3, WS_OUT3, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_BAND, WS_COUNT_
 };
 
 struct Ctx {
@@ -219,8 +219,22 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);
 void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
 
-// Host Huffman (huffman_host.cpp)
-void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out);
+// Host Huffman (huffman_host.cpp). n = the block's size: below kBandCeil the tie-break follows
+// the reference's heap history (heap_order.cpp); n = 0 takes the closed-form order.
+void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out, uint64_t n = 0);
+
+// The reference's BTree address order for small blocks (heap_order.cpp): per leaf count L,
+// off[L] = first entry of L's 2L - 1 node ranks in `rank`, or kModelOrder where the
+// closed-form order holds. band_ranks(n) is nullptr when it holds for every
+// L (always for n >= kBandCeil); results are cached per n, process-wide.
+constexpr uint64_t kBandCeil = 1u << 17;
+constexpr uint32_t kModelOrder = 0xffffffffu;
+struct BandRanks {
+    std::vector<uint32_t> off;   // 257 entries
+    std::vector<uint16_t> rank;  // node id -> ascending-address rank among the 2L - 1 nodes
+};
+const BandRanks *band_ranks(uint64_t n);
+void node_ranks(uint64_t n, uint32_t L, uint16_t *rank);  // exact ranks (model or heap history)
 uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);
 
 // Device Huffman decode table of one record (built on the host by build_dec_table).

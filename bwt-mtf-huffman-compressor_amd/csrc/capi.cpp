@@ -932,6 +932,27 @@ bmh_status bmh_huffman_build(const uint64_t freq[256], const uint64_t first[256]
     API_END
 }
 
+bmh_status bmh_huffman_build_sized(const uint64_t freq[256], const uint64_t first[256], uint64_t n,
+                                   bmh_code_table *out)
+{
+    API_BEGIN
+    if (!freq || !first || !out) fail(BMH_EINVAL, "null argument");
+    huffman_build(freq, first, out, n);
+    API_END
+}
+
+int bmh_node_ranks(uint64_t n, uint32_t L, uint16_t *rank)
+{
+    if (!rank || L == 0 || L > 256) return -1;
+    try {
+        node_ranks(n, L, rank);
+        const BandRanks *br = band_ranks(n);
+        return br && br->off[L] != kModelOrder ? 1 : 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
 uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
 {
     return (t && freq) ? payload_bytes(t, freq) : 0;

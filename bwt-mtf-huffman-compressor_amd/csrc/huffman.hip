@@ -9,7 +9,9 @@
 //              0..L-1, internal nodes L, L+1, ... in creation order; a pop takes the
 //              smallest (freq, -addr_rank(id)) — equal frequencies leave the heap in
 //              descending glibc heap-address order (same model as
-//              huffman_host.cpp) — run as two queues (sorted leaves, internal-node groups).
+//              huffman_host.cpp) — run as two queues (sorted leaves, internal-node groups);
+//              blocks below 128 KiB whose order follows the reference's heap history instead
+//              (heap_order.cpp) pop by wave-wide minimum over per-node keys.
 //   codes    : pointer jumping on parent links (left = 0); preorder tree bits (internal 1,
 //              leaf 0 + 8 value bits MSB-first) placed per leaf in parallel.
 //   header   : [u64 primary][u64 n][u64 tree_len][tree bytes] staged per block.
@@ -77,7 +79,8 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ prim, const uint64_t *__restrict__ boffs,
                                                    DevTable *__restrict__ tabs, uint8_t *__restrict__ hdr,
                                                    uint32_t *__restrict__ hdr_len, uint64_t *__restrict__ pay_bytes,
-                                                   uint32_t *status)
+                                                   uint32_t *status, const uint32_t *__restrict__ rbase,
+                                                   const uint32_t *__restrict__ ridx, const uint16_t *__restrict__ rrank)
 {
     __shared__ uint32_t s_freq[256], s_first[256];
     __shared__ uint8_t s_order[256];
@@ -119,6 +122,54 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         if (lane == 0) atomicOr(status, kStatusEmpty);
         return;
     }
+    // small blocks whose node addresses follow the reference's heap history (heap_order.cpp):
+    // ro = the first of this L's 2L - 1 ranks, or kModelOrder (the closed form holds)
+    uint32_t ro = kModelOrder;
+    if (rbase) {
+        const uint32_t rb = rbase[b];
+        if (rb != kModelOrder) ro = ridx[rb + L];
+    }
+    if (ro != kModelOrder) {
+        // the internal nodes' ranks need not ascend, so the queue is simulated as it is: every
+        // live node's key in a register slot (node v: lane v & 63, slot v >> 6), each pop a
+        // wave-wide minimum (smallest frequency, then the larger address rank)
+        const uint16_t *rk = rrank + ro;
+        uint64_t key[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t id = lane + 64 * k;
+            key[k] = id < L ? ((uint64_t)s_freq[s_order[id]] << 32) | ((0xffffu - rk[id]) << 16) | id : ~0ull;
+        }
+        for (uint32_t m = 0; m + 1 < L; ++m) {
+            uint64_t r[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                uint64_t mn = key[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k) mn = key[k] < mn ? key[k] : mn;
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const uint64_t o = __shfl_xor(mn, off, 64);
+                    mn = o < mn ? o : mn;
+                }
+                r[t] = mn;
+                const uint32_t id = (uint32_t)(mn & 0xffffu);
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k)
+                    if (lane + 64 * k == id) key[k] = ~0ull;
+            }
+            const uint32_t v = L + m;
+            const uint64_t f = (r[0] >> 32) + (r[1] >> 32);
+            if (lane == 0) {
+                s_left[v] = (int16_t)(r[0] & 0xffffu);
+                s_right[v] = (int16_t)(r[1] & 0xffffu);
+            }
+            const uint64_t nk = (f << 32) | ((0xffffu - rk[v]) << 16) | v;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                if (lane + 64 * k == v) key[k] = nk;
+        }
+    } else {
     // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
     // two queues: the leaves sorted by key, and the internal nodes, which are created with
     // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is
@@ -181,6 +232,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 s_q2[me++] = nk;  // a later group
             }
         }
+    }
     }
     __syncthreads();
     // codes (left 0, right 1; a root leaf gets the empty code) by pointer jumping on parent
@@ -351,8 +403,49 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
     uint8_t *d_hdr = (uint8_t *)c->get(WS_HDR, (size_t)nb * kHdrStride + (size_t)nb * 12 + 64);
     uint64_t *d_payb = (uint64_t *)(d_hdr + (size_t)nb * kHdrStride);
     uint32_t *d_hlen = (uint32_t *)(d_payb + nb);
+    // heap-history node ranks of the blocks below kBandCeil whose order differs from the closed
+    // form for some leaf count (heap_order.cpp), uploaded once per batch layout: rbase[nb] | per
+    // distinct size a 257-entry index (first u16 rank of each L, or kModelOrder) | u16 ranks
+    const uint32_t *d_rbase = nullptr, *d_ridx = nullptr;
+    const uint16_t *d_rrank = nullptr;
+    const uint64_t bsig = layout_sig(3, bt.offs, 0);
+    if (c->ws_tag[WS_BAND] != bsig) {
+        std::vector<uint32_t> rbase(nb, kModelOrder), idx;
+        std::vector<uint16_t> ranks;
+        std::map<uint64_t, uint32_t> seen;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint64_t n = bt.offs[b + 1] - bt.offs[b];
+            const BandRanks *br = band_ranks(n);
+            if (!br) continue;
+            auto it = seen.find(n);
+            if (it == seen.end()) {
+                const uint32_t at = (uint32_t)idx.size();
+                for (uint32_t L = 0; L <= 256; ++L)
+                    idx.push_back(br->off[L] == kModelOrder ? kModelOrder : (uint32_t)ranks.size() + br->off[L]);
+                ranks.insert(ranks.end(), br->rank.begin(), br->rank.end());
+                it = seen.emplace(n, at).first;
+            }
+            rbase[b] = it->second;
+        }
+        c->ws_aux[WS_BAND][0] = idx.empty() ? 0u : 1u;
+        c->ws_aux[WS_BAND][1] = (uint32_t)idx.size();
+        if (!idx.empty()) {
+            const size_t bytes = (rbase.size() + idx.size()) * 4 + ranks.size() * 2;
+            std::vector<uint8_t> h(bytes);
+            memcpy(h.data(), rbase.data(), rbase.size() * 4);
+            memcpy(h.data() + rbase.size() * 4, idx.data(), idx.size() * 4);
+            memcpy(h.data() + (rbase.size() + idx.size()) * 4, ranks.data(), ranks.size() * 2);
+            c->h2d(c->get(WS_BAND, bytes + 64), h.data(), bytes);
+        }
+        c->ws_tag[WS_BAND] = bsig;
+    }
+    if (c->ws_aux[WS_BAND][0]) {
+        d_rbase = (const uint32_t *)c->ws[WS_BAND];
+        d_ridx = d_rbase + nb;
+        d_rrank = (const uint16_t *)(d_ridx + c->ws_aux[WS_BAND][1]);
+    }
     BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
-               d_status);
+               d_status, d_rbase, d_ridx, d_rrank);
     const uint64_t *d_base = nullptr;
     if (chain && sub > 0) {
         std::unique_lock<std::mutex> lk(chain->m);

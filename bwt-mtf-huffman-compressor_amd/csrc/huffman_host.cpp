@@ -9,7 +9,8 @@
 // addresses come from glibc malloc in a standalone COMPRESS run; SURVEY.md Appendix B.3
 // gives their ascending order as a function of the leaf count L (node ids: leaves 0..L-1
 // in first-occurrence order of the MTF stream, internal nodes L, L+1, ... in creation
-// order). addr_index() below maps a node id to its position in that order.
+// order). addr_index() below maps a node id to its position in that order; below kBandCeil
+// bytes the order comes from the reference's heap history instead (heap_order.cpp).
 #include "bmh_internal.h"
 
 #include <algorithm>
@@ -48,7 +49,7 @@ struct Node {
 
 }  // namespace
 
-void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out)
+void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out, uint64_t n)
 {
     memset(out, 0, sizeof *out);
     // leaves in first-occurrence order (main.cpp:238-244)
@@ -61,9 +62,14 @@ void huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code
 
     Node nd[511];
     uint32_t nn = 0;
+    // address ranks: the reference's heap history below kBandCeil (heap_order.cpp), else the
+    // closed form
+    uint16_t rank[511];
+    const bool hist = n != 0 && n < kBandCeil;
+    if (hist) node_ranks(n, L, rank);
     auto pops_first = [&](uint32_t a, uint32_t b) {  // true if node a leaves the queue before b
         if (nd[a].freq != nd[b].freq) return nd[a].freq < nd[b].freq;
-        return addr_index(L, a) > addr_index(L, b);
+        return hist ? rank[a] > rank[b] : addr_index(L, a) > addr_index(L, b);
     };
     auto cmp = [&](uint32_t a, uint32_t b) { return pops_first(b, a); };  // max-heap on pops_first
     std::priority_queue<uint32_t, std::vector<uint32_t>, decltype(cmp)> pq(cmp);

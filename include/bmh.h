@@ -94,6 +94,17 @@ bmh_status bmh_histogram_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *
  * first occurrence; equal frequencies break ties by the reference's heap-address order
  * under glibc. */
 bmh_status bmh_huffman_build(const uint64_t freq[256], const uint64_t first[256], bmh_code_table *out);
+/* The same for a block of n bytes: below 128 KiB the tie-break follows the heap history of a
+ * standalone reference COMPRESS run of n bytes (glibc 2.35; the `new BTree` addresses of
+ * main.cpp:240,252 depend on the blocks read_bytes / bwt / move_to_front freed before,
+ * io_utilities.h:40-54, main.cpp:77-112), which decides the records of the small-input bands
+ * (SURVEY §8(f) row 4). bmh_encode_blocks_dev applies the same order per block. */
+bmh_status bmh_huffman_build_sized(const uint64_t freq[256], const uint64_t first[256], uint64_t n,
+                                   bmh_code_table *out);
+/* Node address ranks the above uses for n bytes and L leaves: rank[s] for node ids s < 2L - 1
+ * (leaves by first occurrence, then internal nodes in creation order). Returns 1 when they
+ * come from the heap history, 0 when the closed-form order of SURVEY App. B.3 holds. */
+int bmh_node_ranks(uint64_t n, uint32_t L, uint16_t *rank);
 /* Payload bytes encode_with_huffman (main.cpp:158-172) emits: max(1, ceil(sum freq*len / 8)). */
 uint64_t bmh_payload_bytes(const bmh_code_table *table, const uint64_t freq[256]);
 
