@@ -234,6 +234,7 @@ struct BandRanks {
     std::vector<uint16_t> rank;  // node id -> ascending-address rank among the 2L - 1 nodes
 };
 const BandRanks *band_ranks(uint64_t n);
+void band_ranks_prefetch(const std::vector<uint64_t> &sizes);  // computes the missing ones in parallel
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank);  // exact ranks (model or heap history)
 uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);
 

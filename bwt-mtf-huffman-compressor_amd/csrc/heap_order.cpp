@@ -18,9 +18,12 @@
 // (oracle/alloc_trace) and byte for byte against its records in the bands (tests/test_bands.py).
 #include "bmh_internal.h"
 
-#include <map>
+#include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
+#include <thread>
 #include <unordered_map>
 
 namespace bmh {
@@ -56,11 +59,41 @@ struct HeapSim {
         uint64_t size;
         int32_t bin;  // -1: allocated, in a tcache bin or a fastbin (inuse bit set); else its bin
     };
-    std::map<uint64_t, Chunk> ch;       // every chunk carved from the heap (top excluded)
+    // every chunk carved from the heap (top excluded), by address: a sorted vector (a few
+    // hundred entries; copied once per leaf count by compute_band_ranks)
+    struct Map {
+        std::vector<std::pair<uint64_t, Chunk>> v;
+        using It = std::vector<std::pair<uint64_t, Chunk>>::iterator;
+        It lb(uint64_t a)
+        {
+            return std::lower_bound(v.begin(), v.end(), a,
+                                    [](const std::pair<uint64_t, Chunk> &e, uint64_t x) { return e.first < x; });
+        }
+        It find(uint64_t a)
+        {
+            It it = lb(a);
+            return it != v.end() && it->first == a ? it : v.end();
+        }
+        It begin() { return v.begin(); }
+        It end() { return v.end(); }
+        Chunk &at(uint64_t a)
+        {
+            It it = find(a);
+            if (it == v.end()) throw std::logic_error("heap_order: no chunk");
+            return it->second;
+        }
+        Chunk &operator[](uint64_t a)
+        {
+            It it = lb(a);
+            if (it == v.end() || it->first != a) it = v.insert(it, {a, Chunk{0, -1}});
+            return it->second;
+        }
+        It erase(It it) { return v.erase(it); }
+    } ch;
     std::vector<uint64_t> bins[128];    // unsorted (1), small, large; head (fd side) first
     std::vector<uint64_t> tc[kTcBins];  // back = head
     std::vector<uint64_t> fb[10];       // back = head
-    std::unordered_map<uint64_t, uint64_t> mm;  // mmapped blocks: mem -> chunk size
+    std::vector<std::pair<uint64_t, uint64_t>> mm;  // mmapped blocks: (mem, chunk size)
     bool have_fast = false, tc_ready = false;
     uint64_t top = 0, top_size = 0, last_rem = ~0ull, mm_next = kMmapBase;
     uint64_t mmap_thr = 128 * 1024, trim_thr = 128 * 1024;
@@ -123,7 +156,7 @@ struct HeapSim {
             const uint64_t sz = (nb + kSizeSz + kPage - 1) & ~(kPage - 1);
             const uint64_t mem = mm_next + 16;
             mm_next += sz + kPage;
-            mm[mem] = sz;
+            mm.push_back({mem, sz});
             return mem;
         }
         const uint64_t size = (nb + kTopPad + kMinSize - top_size + kPage - 1) & ~(kPage - 1);
@@ -300,7 +333,7 @@ struct HeapSim {
 
     void free(uint64_t mem)
     {
-        auto m = mm.find(mem);
+        auto m = std::find_if(mm.begin(), mm.end(), [&](const std::pair<uint64_t, uint64_t> &e) { return e.first == mem; });
         if (m != mm.end()) {
             const uint64_t sz = m->second;
             mm.erase(m);
@@ -382,6 +415,16 @@ uint32_t model_index(uint32_t L, uint32_t s)
     return s;
 }
 
+// No free block can serve a 24-byte request: the top serves the next ones in address order
+// (a top too small for one is extended in place: the brk heap is contiguous).
+bool top_only(const HeapSim &h)
+{
+    if (!h.tc[0].empty() || !h.fb[0].empty()) return false;
+    for (uint32_t i = 1; i < 128; ++i)
+        if (!h.bins[i].empty()) return false;
+    return true;
+}
+
 std::unique_ptr<BandRanks> compute_band_ranks(uint64_t n)
 {
     auto out = std::make_unique<BandRanks>();
@@ -402,8 +445,12 @@ std::unique_ptr<BandRanks> compute_band_ranks(uint64_t n)
             cap = nc;
         }
         const uint32_t L = i + 1, nn = 2 * L - 1;
-        HeapSim s = h;
-        for (uint32_t j = L; j < nn; ++j) addr[j] = s.malloc(24);  // internal nodes (main.cpp:252)
+        if (top_only(h)) {  // every internal node is carved from the top, one after another
+            for (uint32_t j = L; j < nn; ++j) addr[j] = h.top + 16 + 32 * (uint64_t)(j - L);
+        } else {
+            HeapSim s = h;
+            for (uint32_t j = L; j < nn; ++j) addr[j] = s.malloc(24);  // internal nodes (main.cpp:252)
+        }
         uint16_t idx[511];
         for (uint32_t j = 0; j < nn; ++j) idx[j] = (uint16_t)j;
         std::sort(idx, idx + nn, [&](uint16_t a, uint16_t b) { return addr[a] < addr[b]; });
@@ -431,10 +478,40 @@ std::unordered_map<uint64_t, std::unique_ptr<BandRanks>> g_band;
 const BandRanks *band_ranks(uint64_t n)
 {
     if (n == 0 || n >= kBandCeil) return nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_band_mu);
+        auto it = g_band.find(n);
+        if (it != g_band.end()) return it->second.get();
+    }
+    auto r = compute_band_ranks(n);  // outside the lock: other sizes proceed meanwhile
     std::lock_guard<std::mutex> lk(g_band_mu);
     auto it = g_band.find(n);
-    if (it == g_band.end()) it = g_band.emplace(n, compute_band_ranks(n)).first;
+    if (it == g_band.end()) it = g_band.emplace(n, std::move(r)).first;
     return it->second.get();
+}
+
+void band_ranks_prefetch(const std::vector<uint64_t> &sizes)
+{
+    std::vector<uint64_t> todo;
+    {
+        std::lock_guard<std::mutex> lk(g_band_mu);
+        for (uint64_t n : sizes)
+            if (n && n < kBandCeil && !g_band.count(n)) todo.push_back(n);
+    }
+    std::sort(todo.begin(), todo.end());
+    todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
+    if (todo.size() < 2) {
+        for (uint64_t n : todo) band_ranks(n);
+        return;
+    }
+    const unsigned nt = std::min<unsigned>((unsigned)todo.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&] {
+            for (size_t i; (i = next.fetch_add(1)) < todo.size();) band_ranks(todo[i]);
+        });
+    for (auto &x : th) x.join();
 }
 
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank)

@@ -413,6 +413,12 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         std::vector<uint32_t> rbase(nb, kModelOrder), idx;
         std::vector<uint16_t> ranks;
         std::map<uint64_t, uint32_t> seen;
+        {
+            std::vector<uint64_t> sizes;
+            for (uint32_t b = 0; b < nb; ++b)
+                if (bt.offs[b + 1] - bt.offs[b] < kBandCeil) sizes.push_back(bt.offs[b + 1] - bt.offs[b]);
+            band_ranks_prefetch(sizes);
+        }
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t n = bt.offs[b + 1] - bt.offs[b];
             const BandRanks *br = band_ranks(n);
