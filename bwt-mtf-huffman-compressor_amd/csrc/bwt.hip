@@ -81,6 +81,7 @@ constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register b
 constexpr uint32_t kBigCapLarge = 4096, kBigCapSmall = 19072, kBigNT = 1024;
 constexpr uint64_t kBigCapLargeBatch = 8ull << 20;  // batches of more bytes use kBigCapLarge
 constexpr uint64_t kFullSaBatch = 16ull << 20;      // batches up to this size store the full SA
+constexpr uint64_t kMergeSortBatch = 16ull << 20;   // ... and launch two bitonic list classes a round
 static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kSegCap && kSegCap <= kDenseCap, "list classes");
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
@@ -2741,6 +2742,10 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     // one partial tile per segment
     const size_t bcap = ccap[kListBig], dtcap = N / kDTile + bcap + 2;
     static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
+    // bitonic list classes merged into two launches per round for latency-bound batches
+    // (BMH_SORT_CLASSES=5 keeps the five shapes: an A/B knob)
+    static const int sort_classes = getenv("BMH_SORT_CLASSES") ? atoi(getenv("BMH_SORT_CLASSES")) : 0;
+    const bool merge_sort_classes = sort_classes == 2 || (sort_classes == 0 && N <= kMergeSortBatch);
 
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
@@ -2872,6 +2877,18 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                 const uint32_t fm = h_cnt->lc[in][4][0];
                 const uint32_t gf = 8u * rows[kListFin], gw = 8u * cdiv(rows[kListFin], 4);
                 const uint32_t *lof = d_loff + kListFin * 9, *cf = dc + kListFin * 8;
+                if (merge_sort_classes) {
+                    // latency-bound batches: two launches per round instead of up to five (each
+                    // network is sized to its segment, so the wider shapes sort the shorter
+                    // segments of their range with the same stages; the launches of one stream
+                    // run one after another, so fewer of them shorten the round)
+                    if (fm & 3u)
+                        BMH_LAUNCH(c, "bwt_finish", (k_finish_sortw<8, 4>), gw, 256, 0, da, lf[in], lof, cf, 1u,
+                                   lm[kListFin]);
+                    if (fm & 28u)
+                        BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<512, 8>), gf, 512, 0, da, lf[in], lof, cf, 512u,
+                                   lm[kListFin]);
+                } else {
                 if (fm & 1u)
                     BMH_LAUNCH(c, "bwt_finish", (k_finish_sortw<2, 4>), gw, 256, 0, da, lf[in], lof, cf, 1u, lm[kListFin]);
                 if (fm & 2u)
@@ -2885,6 +2902,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                 if (fm & 16u)
                     BMH_LAUNCH(c, "bwt_finish", (k_finish_sort<512, 8>), gf, 512, 0, da, lf[in], lof, cf, 2048u,
                                lm[kListFin]);
+                }
             }
             if (tot[kListFinb]) {  // counting-sort finish: dense shape, or 1024 threads up to kBigCapSmall
                 if (big_cap > kSegCap)
