@@ -2132,13 +2132,10 @@ __device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32
     }
 }
 
-__global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 *__restrict__ tiny,
-                           uint2 *__restrict__ med, LSeg *__restrict__ large, Counters *cnt,
-                           const uint32_t *__restrict__ boffs, uint32_t nb)
+__device__ __forceinline__ void classify_one(const uint2 s, uint2 *__restrict__ tiny, uint2 *__restrict__ med,
+                                             LSeg *__restrict__ large, Counters *cnt, const uint32_t *__restrict__ boffs,
+                                             uint32_t nb)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nseg) return;
-    const uint2 s = segs[i];
     if (s.y <= kTinyMax) {
         tiny[wave_append(&cnt->tiny)] = s;
     } else if (s.y <= kMedMax) {
@@ -2153,6 +2150,17 @@ __global__ void k_classify(const uint2 *__restrict__ segs, uint32_t nseg, uint2 
         l.gathered = 0;
         large[wave_append(&cnt->large)] = l;
     }
+}
+
+// Grid-stride over the nseg_p[0] segments the previous round left (read on the device: the
+// host learns the class counts from the same wait that gives it the segment count).
+__global__ void k_classify(const uint2 *__restrict__ segs, const uint32_t *__restrict__ nseg_p, uint2 *__restrict__ tiny,
+                           uint2 *__restrict__ med, LSeg *__restrict__ large, Counters *cnt,
+                           const uint32_t *__restrict__ boffs, uint32_t nb)
+{
+    const uint32_t nseg = *nseg_p;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nseg; i += gridDim.x * blockDim.x)
+        classify_one(segs[i], tiny, med, large, cnt, boffs, nb);
 }
 
 // Tiles of <= kDTile slots over a segment list whose length is on the device: one workgroup
@@ -2987,6 +2995,17 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         BMH_LAUNCH(c, "bwt_group_fill", k_group_fill, std::min<uint32_t>(cdiv(ngroups, 256), 65536), 256, 0, da, dgroups,
                    ngroups, rkA, rkB, seg_cur, coop, d_cnt);
         BMH_LAUNCH(c, "bwt_group_fill", k_group_fill_coop, kCoopGrid, 256, 0, da, dgroups, coop, rkA, rkB, seg_cur, d_cnt);
+        // each round's segments are classified at the end of the round before (here: of the
+        // fill), so the one host wait per round also says which segment classes the next one
+        // holds and the launches of empty classes are skipped (each costs a few microseconds of
+        // a latency-bound round: up to 5 per MSD pass)
+        const uint32_t cgrid = std::min<uint32_t>(cdiv(seg_cap, 256), 256);
+        auto classify = [&](const uint2 *segs) {
+            BMH_HIP(hipMemsetAsync(d_cnt, 0, 3 * 4, c->stream));  // tiny, med, large
+            BMH_LAUNCH(c, "bwt_classify", k_classify, cgrid, 256, 0, segs, &d_cnt->next, tiny, med, large, d_cnt,
+                       d_boffs, nb);
+        };
+        classify(seg_cur);
         read_counters();
         uint32_t ncur = h_cnt->next;
         uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
@@ -3012,11 +3031,11 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             a.resolved = resolved;
             a.cnt = d_cnt;
 
-            BMH_HIP(hipMemsetAsync(d_cnt, 0, 8 * 4, c->stream));  // the 8 doubling-phase counters
+            // the doubling-phase counters but the class counts classify() just wrote
+            BMH_HIP(hipMemsetAsync(&d_cnt->large_next, 0, 5 * 4, c->stream));
             BMH_HIP(hipMemsetAsync(&d_cnt->coop_groups, 0, 4, c->stream));
-            BMH_LAUNCH(c, "bwt_classify", k_classify, cdiv(ncur, 256), 256, 0, seg_cur, ncur, tiny, med, large, d_cnt,
-                       d_boffs, nb);
-            for (uint32_t pass = 0; pass < npass; ++pass) {  // passes with no segments exit at once
+            const bool has_large = h_cnt->large != 0;  // the large path also appends tiny / medium segments
+            for (uint32_t pass = 0; has_large && pass < npass; ++pass) {  // passes with no segments exit at once
                 uint32_t *cnt_in = pass & 1 ? &d_cnt->large_next : &d_cnt->large;
                 uint32_t *cnt_out = pass & 1 ? &d_cnt->large : &d_cnt->large_next;
                 LSeg *lin = pass & 1 ? large2 : large, *lout = pass & 1 ? large : large2;
@@ -3031,12 +3050,13 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                 BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, kDblGrid, 256, 0, d_ltiles, &d_cnt->ltiles, d_lnomove, sa, key, sa2,
                            key2);
             }
-            BMH_LAUNCH(c, "bwt_tiny", k_dtiny, kDblGrid, 256, 0, a, tiny);
-            BMH_LAUNCH(c, "bwt_medium", k_medium, kDblGrid, kMedNT, 0, a, med);
+            if (has_large || h_cnt->tiny) BMH_LAUNCH(c, "bwt_tiny", k_dtiny, kDblGrid, 256, 0, a, tiny);
+            if (has_large || h_cnt->med) BMH_LAUNCH(c, "bwt_medium", k_medium, kDblGrid, kMedNT, 0, a, med);
             BMH_LAUNCH(c, "bwt_groups", k_groups, kDblGrid, 256, 0, a, groups, gcoop);
             BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
             BMH_LAUNCH(c, "bwt_commit", k_commit, kDblGrid, 256, 0, resolved, &d_cnt->resolved, a.rk_nxt,
                        (uint32_t *)a.rk_cur);
+            classify(seg_nxt);
             read_counters();
             ncur = h_cnt->next;
             std::swap(seg_cur, seg_nxt);
