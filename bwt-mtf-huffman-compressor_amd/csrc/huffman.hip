@@ -135,10 +135,13 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         // wave-wide minimum (smallest frequency, then the larger address rank)
         const uint16_t *rk = rrank + ro;
         uint64_t key[8];
+        uint32_t rkr[8];  // the ranks of this lane's nodes (id = lane + 64 k), all loads at once
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) rkr[k] = lane + 64 * k < 2 * L - 1 ? rk[lane + 64 * k] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
             const uint32_t id = lane + 64 * k;
-            key[k] = id < L ? ((uint64_t)s_freq[s_order[id]] << 32) | ((0xffffu - rk[id]) << 16) | id : ~0ull;
+            key[k] = id < L ? ((uint64_t)s_freq[s_order[id]] << 32) | ((0xffffu - rkr[k]) << 16) | id : ~0ull;
         }
         for (uint32_t m = 0; m + 1 < L; ++m) {
             uint64_t r[2];
@@ -164,10 +167,9 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 s_left[v] = (int16_t)(r[0] & 0xffffu);
                 s_right[v] = (int16_t)(r[1] & 0xffffu);
             }
-            const uint64_t nk = (f << 32) | ((0xffffu - rk[v]) << 16) | v;
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k)
-                if (lane + 64 * k == v) key[k] = nk;
+            for (uint32_t k = 0; k < 8; ++k)  // the owning lane builds the new node's key
+                if (lane + 64 * k == v) key[k] = (f << 32) | ((0xffffu - rkr[k]) << 16) | v;
         }
     } else {
     // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
@@ -188,28 +190,35 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     if (lane == 0) {
         uint32_t q1 = 0;                      // next leaf
         uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
-        uint64_t k1 = s_k1[0], k2 = ~0ull;    // queue heads (k2 = s_q2[ge - 1])
+        // queue heads kept in registers with the entry behind each (its LDS read is issued a pop
+        // ahead of its use): k1 = s_k1[q1], k1n = s_k1[q1 + 1]; k2 = s_q2[ge - 1], k2b =
+        // s_q2[ge - 2] while that is still in the first group (else ~0)
+        uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k2 = ~0ull, k2b = ~0ull;
         uint32_t gf = 0;                      // first group's frequency
         auto pop = [&]() -> uint64_t {
             uint64_t r;
             if (k1 < k2) {
                 r = k1;
                 ++q1;
-                k1 = q1 < L ? s_k1[q1] : ~0ull;
+                k1 = k1n;
+                k1n = q1 + 1 < L ? s_k1[q1 + 1] : ~0ull;
             } else {
                 r = k2;
                 --ge;
                 if (ge > gh) {
-                    k2 = s_q2[ge - 1];
+                    k2 = k2b;
+                    k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
                 } else {  // the first group is used up: the next one starts at gn
                     gh = gn;
                     ge = gh;
                     k2 = ~0ull;
+                    k2b = ~0ull;
                     if (gh < me) {
                         gf = (uint32_t)(s_q2[gh] >> 32);
                         while (ge < me && (uint32_t)(s_q2[ge] >> 32) == gf) ++ge;
                         gn = ge;
                         k2 = s_q2[ge - 1];
+                        k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
                     }
                 }
             }
@@ -225,6 +234,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
             if (gn == me && (ge == gh || (uint32_t)f == gf)) {
                 // the queue is empty, or the node joins the last (= first) group: it pops first
                 if (ge == gh) gf = (uint32_t)f;
+                k2b = ge == gh ? ~0ull : k2;  // the old head is now the second
                 s_q2[ge++] = nk;
                 if (ge > gn) gn = me = ge;
                 k2 = nk;
