@@ -135,6 +135,8 @@ struct Counters {
     uint32_t ltiles;                  // tiles of the current large-path MSD pass (k_tiles)
     uint32_t tstart[9];               // data-phase MSD tiles of each XCD lane (k_dtiles)
     uint32_t g1next[8];               // persistent global pass: chunks handed out per XCD lane
+    uint32_t next2;                   // doubling rounds: next / next2 hold the segments of
+                                      // alternate rounds (the one a round appends to is zero)
 };
 // Workgroup lanes -> list sub-lists of one launch: workgroup i runs on XCD i mod 8 (v = i & 7);
 // the 8 values of v are dealt over the non-empty sub-lists (a batch of few blocks fills few
@@ -2102,6 +2104,7 @@ struct RoundArgs {
     uint2 *next;
     uint32_t *resolved;  // positions resolved this round (batch index of p) -> committed after
     Counters *cnt;
+    uint32_t *next_cnt;  // entries of `next` (cnt->next or cnt->next2, alternating by round)
 };
 
 __device__ __forceinline__ uint32_t round_key(const RoundArgs &a, uint32_t boff, uint32_t n, uint32_t p)
@@ -2127,7 +2130,7 @@ __device__ __forceinline__ void finish(const RoundArgs &a, uint32_t boff, uint32
             a.prim[b] = gs;
         }
     } else if (first) {
-        const uint32_t i = wave_append(&a.cnt->next);
+        const uint32_t i = wave_append(a.next_cnt);
         a.next[i] = make_uint2(boff + gs, gsz);
     }
 }
@@ -2584,6 +2587,19 @@ __global__ void k_commit(const uint32_t *__restrict__ list, const uint32_t *__re
         dst[list[i]] = src[list[i]];
 }
 
+// End of a doubling round (or of the group fill): the per-round counters zeroed for the next
+// one in one launch (class counts before k_classify rebuilds them; `zero_next` = the segment
+// count the next round appends to, i.e. the one this round read).
+__global__ void k_dbl_reset(Counters *cnt, uint32_t *zero_next)
+{
+    if (threadIdx.x == 0) {
+        cnt->tiny = cnt->med = cnt->large = 0;
+        cnt->large_next = cnt->groups = cnt->tiles = cnt->resolved = 0;
+        cnt->coop_groups = 0;
+        *zero_next = 0;
+    }
+}
+
 __global__ void k_fill_u32(uint32_t *p, uint32_t v, uint32_t n)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2999,13 +3015,17 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         // fill), so the one host wait per round also says which segment classes the next one
         // holds and the launches of empty classes are skipped (each costs a few microseconds of
         // a latency-bound round: up to 5 per MSD pass)
+        // round r reads the segment count of counter in(r) and appends to out(r): next / next2
+        // alternate (the fill wrote next), so the reset at the end of a round zeroes the count
+        // it read and nothing is zeroed at the start of the next
         const uint32_t cgrid = std::min<uint32_t>(cdiv(seg_cap, 256), 256);
-        auto classify = [&](const uint2 *segs) {
-            BMH_HIP(hipMemsetAsync(d_cnt, 0, 3 * 4, c->stream));  // tiny, med, large
-            BMH_LAUNCH(c, "bwt_classify", k_classify, cgrid, 256, 0, segs, &d_cnt->next, tiny, med, large, d_cnt,
-                       d_boffs, nb);
+        auto cnt_of = [&](int r) { return (r & 1) ? &d_cnt->next2 : &d_cnt->next; };  // in(r); out(r) = in(r + 1)
+        auto classify = [&](const uint2 *segs, int r, uint32_t *zero_next) {  // segs: round r's input
+            BMH_LAUNCH(c, "bwt_classify", k_dbl_reset, 1, 64, 0, d_cnt, zero_next);
+            BMH_LAUNCH(c, "bwt_classify", k_classify, cgrid, 256, 0, segs, cnt_of(r), tiny, med, large, d_cnt, d_boffs,
+                       nb);
         };
-        classify(seg_cur);
+        classify(seg_cur, 0, cnt_of(1));
         read_counters();
         uint32_t ncur = h_cnt->next;
         uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
@@ -3030,10 +3050,8 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             a.next = seg_nxt;
             a.resolved = resolved;
             a.cnt = d_cnt;
+            a.next_cnt = cnt_of(round + 1);
 
-            // the doubling-phase counters but the class counts classify() just wrote
-            BMH_HIP(hipMemsetAsync(&d_cnt->large_next, 0, 5 * 4, c->stream));
-            BMH_HIP(hipMemsetAsync(&d_cnt->coop_groups, 0, 4, c->stream));
             const bool has_large = h_cnt->large != 0;  // the large path also appends tiny / medium segments
             for (uint32_t pass = 0; has_large && pass < npass; ++pass) {  // passes with no segments exit at once
                 uint32_t *cnt_in = pass & 1 ? &d_cnt->large_next : &d_cnt->large;
@@ -3056,9 +3074,9 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
             BMH_LAUNCH(c, "bwt_commit", k_commit, kDblGrid, 256, 0, resolved, &d_cnt->resolved, a.rk_nxt,
                        (uint32_t *)a.rk_cur);
-            classify(seg_nxt);
+            classify(seg_nxt, round + 1, cnt_of(round));
             read_counters();
-            ncur = h_cnt->next;
+            ncur = (round & 1) ? h_cnt->next : h_cnt->next2;  // in(round + 1)
             std::swap(seg_cur, seg_nxt);
             D = a.newD;
             ++round;
