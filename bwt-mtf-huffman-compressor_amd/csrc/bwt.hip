@@ -2600,11 +2600,17 @@ __global__ void k_dbl_reset(Counters *cnt, uint32_t *zero_next)
     }
 }
 
-__global__ void k_fill_u32(uint32_t *p, uint32_t v, uint32_t n)
+// Start of the data phase in one launch: primaries unset, block flags and counters zero.
+__global__ void k_phase_init(uint32_t *prim, uint32_t *bflag, uint32_t nb, uint32_t *cnt, uint32_t ncnt)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) p[i] = v;
+    if (i < nb) {
+        prim[i] = 0xffffffffu;
+        bflag[i] = 0;
+    }
+    if (i < ncnt) cnt[i] = 0;
 }
+
 
 
 // Host-side tiling of a segment list into <= kDTile pieces.
@@ -2783,9 +2789,10 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         da.full_sa = full_sa ? 1u : 0u;
         da.big_cap = big_cap;
         if (kb_cur != rec) std::swap(kb_cur, kb_nxt);  // the global pass writes its windows into rec
-        BMH_HIP(hipMemsetAsync(d_cnt, 0, sizeof(Counters), c->stream));
-        BMH_HIP(hipMemsetAsync(bflag, 0, nb * 4, c->stream));
-        BMH_LAUNCH(c, "bwt_fill", k_fill_u32, cdiv(nb, 256), 256, 0, d_prim, 0xffffffffu, nb);
+        static_assert(sizeof(Counters) % 4 == 0, "counter words");
+        constexpr uint32_t kCntWords = sizeof(Counters) / 4;
+        BMH_LAUNCH(c, "bwt_fill", k_phase_init, cdiv(std::max(nb, kCntWords), 256), 256, 0, d_prim, bflag, nb,
+                   (uint32_t *)d_cnt, kCntWords);
 
         // ---- data phase
         BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
