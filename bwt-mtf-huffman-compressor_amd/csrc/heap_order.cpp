@@ -425,6 +425,39 @@ bool top_only(const HeapSim &h)
     return true;
 }
 
+// k 24-byte allocations from state s (the internal nodes, main.cpp:252; no frees in between),
+// addresses to out. Two runs are carved in address order without the full allocator path: the
+// top, and a last remainder that is the unsorted bin's only chunk (each request splits 32 bytes
+// off it while it is larger than 64: malloc.c's last-remainder rule for small requests). The
+// allocated chunks are not recorded: nothing is freed afterwards.
+void m24_run(HeapSim &s, uint32_t k, uint64_t *out)
+{
+    for (uint32_t j = 0; j < k;) {
+        if (top_only(s)) {
+            for (uint64_t a = s.top + 16; j < k; ++j, a += 32) out[j] = a;
+            return;
+        }
+        if (s.tc[0].empty() && s.fb[0].empty() && s.bins[2].empty() && s.bins[1].size() == 1 &&
+            s.bins[1][0] == s.last_rem) {
+            const uint64_t p0 = s.last_rem;
+            uint64_t p = p0, sz = s.ch.at(p0).size;
+            if (sz > 64) {
+                while (j < k && sz > 64) {
+                    out[j++] = p + 16;
+                    p += 32;
+                    sz -= 32;
+                }
+                s.ch.erase(s.ch.find(p0));
+                s.ch[p] = HeapSim::Chunk{sz, 1};
+                s.bins[1][0] = p;
+                s.last_rem = p;
+                continue;
+            }
+        }
+        out[j++] = s.malloc(24);
+    }
+}
+
 std::unique_ptr<BandRanks> compute_band_ranks(uint64_t n)
 {
     auto out = std::make_unique<BandRanks>();
@@ -449,7 +482,7 @@ std::unique_ptr<BandRanks> compute_band_ranks(uint64_t n)
             for (uint32_t j = L; j < nn; ++j) addr[j] = h.top + 16 + 32 * (uint64_t)(j - L);
         } else {
             HeapSim s = h;
-            for (uint32_t j = L; j < nn; ++j) addr[j] = s.malloc(24);  // internal nodes (main.cpp:252)
+            m24_run(s, nn - L, addr + L);  // internal nodes (main.cpp:252)
         }
         uint16_t idx[511];
         for (uint32_t j = 0; j < nn; ++j) idx[j] = (uint16_t)j;
