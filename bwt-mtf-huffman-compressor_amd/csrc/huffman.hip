@@ -172,77 +172,77 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 if (lane + 64 * k == v) key[k] = (f << 32) | ((0xffffu - rkr[k]) << 16) | v;
         }
     } else {
-    // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
-    // two queues: the leaves sorted by key, and the internal nodes, which are created with
-    // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is
-    // a run of frequency groups, each popped newest first (the larger rank of an equal
-    // frequency pops first). Exactly the heap's pop order, O(1) per pop, on lane 0.
-    for (uint32_t id = lane; id < 256; id += 64) s_lkey[id] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
-    __syncthreads();
-    {
-        uint32_t pos[4];
-        rank4_u64(s_lkey, lane, pos);
+        // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
+        // two queues: the leaves sorted by key, and the internal nodes, which are created with
+        // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is
+        // a run of frequency groups, each popped newest first (the larger rank of an equal
+        // frequency pops first). Exactly the heap's pop order, O(1) per pop, on lane 0.
+        for (uint32_t id = lane; id < 256; id += 64) s_lkey[id] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
+        __syncthreads();
+        {
+            uint32_t pos[4];
+            rank4_u64(s_lkey, lane, pos);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (lane + 64 * k < L) s_k1[pos[k]] = s_lkey[lane + 64 * k];
-    }
-    __syncthreads();
-    if (lane == 0) {
-        uint32_t q1 = 0;                      // next leaf
-        uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
-        // queue heads kept in registers with the entry behind each (its LDS read is issued a pop
-        // ahead of its use): k1 = s_k1[q1], k1n = s_k1[q1 + 1]; k2 = s_q2[ge - 1], k2b =
-        // s_q2[ge - 2] while that is still in the first group (else ~0)
-        uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k2 = ~0ull, k2b = ~0ull;
-        uint32_t gf = 0;                      // first group's frequency
-        auto pop = [&]() -> uint64_t {
-            uint64_t r;
-            if (k1 < k2) {
-                r = k1;
-                ++q1;
-                k1 = k1n;
-                k1n = q1 + 1 < L ? s_k1[q1 + 1] : ~0ull;
-            } else {
-                r = k2;
-                --ge;
-                if (ge > gh) {
-                    k2 = k2b;
-                    k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
-                } else {  // the first group is used up: the next one starts at gn
-                    gh = gn;
-                    ge = gh;
-                    k2 = ~0ull;
-                    k2b = ~0ull;
-                    if (gh < me) {
-                        gf = (uint32_t)(s_q2[gh] >> 32);
-                        while (ge < me && (uint32_t)(s_q2[ge] >> 32) == gf) ++ge;
-                        gn = ge;
-                        k2 = s_q2[ge - 1];
+            for (int k = 0; k < 4; ++k)
+                if (lane + 64 * k < L) s_k1[pos[k]] = s_lkey[lane + 64 * k];
+        }
+        __syncthreads();
+        if (lane == 0) {
+            uint32_t q1 = 0;                      // next leaf
+            uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
+            // queue heads kept in registers with the entry behind each (its LDS read is issued a pop
+            // ahead of its use): k1 = s_k1[q1], k1n = s_k1[q1 + 1]; k2 = s_q2[ge - 1], k2b =
+            // s_q2[ge - 2] while that is still in the first group (else ~0)
+            uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k2 = ~0ull, k2b = ~0ull;
+            uint32_t gf = 0;                      // first group's frequency
+            auto pop = [&]() -> uint64_t {
+                uint64_t r;
+                if (k1 < k2) {
+                    r = k1;
+                    ++q1;
+                    k1 = k1n;
+                    k1n = q1 + 1 < L ? s_k1[q1 + 1] : ~0ull;
+                } else {
+                    r = k2;
+                    --ge;
+                    if (ge > gh) {
+                        k2 = k2b;
                         k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
+                    } else {  // the first group is used up: the next one starts at gn
+                        gh = gn;
+                        ge = gh;
+                        k2 = ~0ull;
+                        k2b = ~0ull;
+                        if (gh < me) {
+                            gf = (uint32_t)(s_q2[gh] >> 32);
+                            while (ge < me && (uint32_t)(s_q2[ge] >> 32) == gf) ++ge;
+                            gn = ge;
+                            k2 = s_q2[ge - 1];
+                            k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
+                        }
                     }
                 }
-            }
-            return r;
-        };
-        for (uint32_t m = 0; m + 1 < L; ++m) {
-            const uint64_t ra = pop(), rb = pop();
-            const uint32_t v = L + m;
-            const uint64_t f = (ra >> 32) + (rb >> 32);
-            s_left[v] = (int16_t)(ra & 0xffffu);
-            s_right[v] = (int16_t)(rb & 0xffffu);
-            const uint64_t nk = heap_key(f, L, v);
-            if (gn == me && (ge == gh || (uint32_t)f == gf)) {
-                // the queue is empty, or the node joins the last (= first) group: it pops first
-                if (ge == gh) gf = (uint32_t)f;
-                k2b = ge == gh ? ~0ull : k2;  // the old head is now the second
-                s_q2[ge++] = nk;
-                if (ge > gn) gn = me = ge;
-                k2 = nk;
-            } else {
-                s_q2[me++] = nk;  // a later group
+                return r;
+            };
+            for (uint32_t m = 0; m + 1 < L; ++m) {
+                const uint64_t ra = pop(), rb = pop();
+                const uint32_t v = L + m;
+                const uint64_t f = (ra >> 32) + (rb >> 32);
+                s_left[v] = (int16_t)(ra & 0xffffu);
+                s_right[v] = (int16_t)(rb & 0xffffu);
+                const uint64_t nk = heap_key(f, L, v);
+                if (gn == me && (ge == gh || (uint32_t)f == gf)) {
+                    // the queue is empty, or the node joins the last (= first) group: it pops first
+                    if (ge == gh) gf = (uint32_t)f;
+                    k2b = ge == gh ? ~0ull : k2;  // the old head is now the second
+                    s_q2[ge++] = nk;
+                    if (ge > gn) gn = me = ge;
+                    k2 = nk;
+                } else {
+                    s_q2[me++] = nk;  // a later group
+                }
             }
         }
-    }
     }
     __syncthreads();
     // codes (left 0, right 1; a root leaf gets the empty code) by pointer jumping on parent
