@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""BASELINE config 5 at full size on one GPU: 8 GiB of Zipf text in 16 MiB blocks
+(512 blocks), streamed from host memory by bmh_compress_host (H2D / encode / D2H overlapped) and,
+when asked, by bmh_compress_host_multi over several contexts (the multi-GPU deal; on a 1-GPU box
+the contexts share device 0). The text is the stream's first 256 MiB repeated (the App. D
+generator is sequential Python, ~7 min for 8 GiB), so blocks 0-15 are the true stream's: blocks
+0-7 are checked record for record against the reference's manifest (zipf_16m). Every block is
+round-tripped by the GPU decoder (bmh_decompress_dev) and compared with the input.
+usage: python tools/config5_run.py [--gib 8] [--contexts 1]"""
+import argparse
+import ctypes as C
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(REPO, "bwt-mtf-huffman-compressor_amd"))
+import bmh  # noqa: E402
+from bmh import synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--gib", type=int, default=8)
+ap.add_argument("--contexts", type=int, default=1)
+a = ap.parse_args()
+n = a.gib << 30
+bs = 16 << 20
+t0 = time.perf_counter()
+data = np.resize(synth.zipf_text(256 << 20), n)
+gen_s = time.perf_counter() - t0
+L = bmh.lib()
+ctxs = [bmh.Context(0) for _ in range(a.contexts)]
+cap = int(L.bmh_compress_bound(n, bs))
+out = np.empty(cap, dtype=np.uint8)
+olen = C.c_uint64()
+
+
+def run():
+    if a.contexts == 1:
+        st = L.bmh_compress_host(ctxs[0].h, data.ctypes.data_as(C.c_void_p), n, bs, out.ctypes.data_as(C.c_void_p),
+                                 cap, C.byref(olen))
+    else:
+        arr = (C.c_void_p * a.contexts)(*[c.h for c in ctxs])
+        st = L.bmh_compress_host_multi(arr, a.contexts, data.ctypes.data_as(C.c_void_p), n, bs,
+                                       out.ctypes.data_as(C.c_void_p), cap, C.byref(olen))
+    if st != 0:
+        raise RuntimeError(L.bmh_last_error().decode())
+
+
+run()  # warm-up
+t1 = time.perf_counter()
+run()
+dt = time.perf_counter() - t1
+rec = out[: olen.value]
+recs = bmh.container_records(rec)
+man = json.load(open(os.path.join(REPO, "tests", "golden", "manifests", "zipf_16m.json")))
+ref_ok = all(hashlib.sha256(recs[i]).hexdigest() == b["sha256"] for i, b in enumerate(man["blocks"]))
+back = np.empty(n, dtype=np.uint8)
+nout = C.c_uint64()
+t2 = time.perf_counter()
+st = L.bmh_decompress_dev(ctxs[0].h, rec.ctypes.data_as(C.c_void_p), rec.size, back.ctypes.data_as(C.c_void_p), n,
+                          C.byref(nout))
+dec_s = time.perf_counter() - t2
+ok = st == 0 and nout.value == n and np.array_equal(back, data)
+print(json.dumps({"config": "5: Zipf text, 16 MiB blocks, host buffers in and out", "GiB": a.gib,
+                  "blocks": len(recs), "contexts": a.contexts, "ms": round(dt * 1e3, 1),
+                  "MBps_pcie_inclusive": round(n / dt / 1e6, 1), "ratio": round(olen.value / n, 6),
+                  "blocks_0_7_equal_reference_manifest": bool(ref_ok), "roundtrip_bit_exact": bool(ok),
+                  "decode_s": round(dec_s, 2), "gen_s": round(gen_s, 1)}))
