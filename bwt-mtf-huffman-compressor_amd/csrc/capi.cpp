@@ -272,17 +272,19 @@ static Ctx *sub_ctx(Ctx *c, size_t i)
     return x;
 }
 
-// Default sub-pipelines: 3 for batches under 128 MiB (their list rounds leave the GPU idle
+// Default sub-pipelines: 3 for batches under 128 MiB of at least 12 blocks (their list rounds leave the GPU idle
 // between host waits, so a third pipeline fills it: Calgary 5.9 -> 5.1 ms, Zipf 100 MB at 1 MiB
 // blocks 11.8 -> 11.1-11.4 ms), 2 above (the 128 MiB text batch, the 256 MiB streamed batches
 // and the 1 GiB headline measured equal or slower with 3; 4+ exceed the device's 4 hardware
 // queues and serialise: Calgary 7.9 ms).
-static int stream_count(Ctx *c, uint64_t total)
+static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
 {
     if (c->nstreams > 0) return c->nstreams;
     const char *e = getenv("BMH_STREAMS");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? std::min(v, 16) : total < (128ull << 20) ? 3 : 2;
+    // (a third pipeline of few, large blocks leaves each with too little work per list round:
+    // 128 MB of Zipf in 8 x 16 MiB blocks 21.35 -> 20.7 ms with 2)
+    return v > 0 ? std::min(v, 16) : total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
 }
 
 // The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
@@ -293,7 +295,7 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
                    uint64_t *rec_offs, int max_pipes)
 {
     const uint32_t nb = bt.nblocks;
-    const int S = (int)std::min<uint32_t>(std::min<uint32_t>((uint32_t)stream_count(c, bt.total), (uint32_t)max_pipes),
+    const int S = (int)std::min<uint32_t>(std::min<uint32_t>((uint32_t)stream_count(c, bt.total, nb), (uint32_t)max_pipes),
                                           nb / 2);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
