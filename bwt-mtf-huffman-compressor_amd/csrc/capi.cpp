@@ -266,7 +266,9 @@ Ctx *aux_ctx(Ctx *c)
 
 static Ctx *sub_ctx(Ctx *c, size_t i)
 {
-    while (c->subs.size() <= i) new_sub(c, nullptr)->aux_stream = c->s_d2h;
+    // a fourth pipeline (BMH_STREAMS=4) runs on stream D, the D2H / run-path side stream, which
+    // device-resident batches past the run screen leave idle; later ones get streams of their own
+    while (c->subs.size() <= i) new_sub(c, c->subs.size() == 3 ? c->s_d2h : nullptr)->aux_stream = c->s_d2h;
     Ctx *x = c->subs[i];
     x->timing = c->timing;
     return x;
@@ -283,8 +285,12 @@ static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
     const char *e = getenv("BMH_STREAMS");
     const int v = e ? atoi(e) : 0;
     // (a third pipeline of few, large blocks leaves each with too little work per list round:
-    // 128 MB of Zipf in 8 x 16 MiB blocks 21.35 -> 20.7 ms with 2)
-    return v > 0 ? std::min(v, 16) : total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
+    // 128 MB of Zipf in 8 x 16 MiB blocks 21.35 -> 20.7 ms with 2). Batches past the run screen
+    // (> 64 MiB) leave stream D idle: four pipelines, one per hardware queue (1 GiB random
+    // 11.08-11.20 -> 10.96-10.98 ms; Zipf 100 MB at 1 MiB blocks 10.94 -> 10.65 ms).
+    if (v > 0) return std::min(v, 16);
+    if (nblocks >= 16 && total > (64ull << 20)) return 4;
+    return total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
 }
 
 // The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
