@@ -26,6 +26,26 @@ namespace {
 
 constexpr uint32_t kHdrStride = 352;  // 24 header bytes + <= 320 tree bytes, 16-aligned
 
+// Phase timing (experiment builds only, -DBMH_PROF_HUFF): lane 0 of each block's wave stores its
+// s_memtime ticks per phase of k_huff_build; codebook_batch prints the means after the launch.
+#ifdef BMH_PROF_HUFF
+__device__ uint32_t g_hprof[4096 * 8];
+#define HPROF_START uint64_t _t0 = __builtin_amdgcn_s_memtime()
+#define HPROF(i)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0) {                                                           \
+            const uint64_t _t = __builtin_amdgcn_s_memtime();                             \
+            if (blockIdx.x < 4096) g_hprof[blockIdx.x * 8 + (i)] = (uint32_t)(_t - _t0); \
+            _t0 = _t;                                                                     \
+        }                                                                                 \
+    } while (0)
+#else
+#define HPROF_START
+#define HPROF(i) \
+    do {         \
+    } while (0)
+#endif
+
 __device__ __forceinline__ uint32_t addr_rank(uint32_t L, uint32_t s)
 {
     if (L <= 128) {
@@ -96,6 +116,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ uint32_t s_err;
     uint8_t *s_tree = (uint8_t *)s_tree32;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    HPROF_START;
     for (uint32_t s = lane; s < 256; s += 64) {
         s_freq[s] = freq32[(size_t)b * 256 + s];
         s_first[s] = first32[(size_t)b * 256 + s];
@@ -122,6 +143,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         if (lane == 0) atomicOr(status, kStatusEmpty);
         return;
     }
+    HPROF(0);  // loads, leaf count, leaf order
     // small blocks whose node addresses follow the reference's heap history (heap_order.cpp):
     // ro = the first of this L's 2L - 1 ranks, or kModelOrder (the closed form holds)
     uint32_t ro = kModelOrder;
@@ -187,6 +209,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 if (lane + 64 * k < L) s_k1[pos[k]] = s_lkey[lane + 64 * k];
         }
         __syncthreads();
+        HPROF(5);  // (model path) leaf keys ranked
         if (lane == 0) {
             uint32_t q1 = 0;                      // next leaf
             uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
@@ -245,6 +268,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         }
     }
     __syncthreads();
+    HPROF(1);  // the queue (merges; key ranking too on the heap-history path)
     // codes (left 0, right 1; a root leaf gets the empty code) by pointer jumping on parent
     // links: node x keeps (target a, path bits c, path length d) with code(x) = code(a) << d | c
     const uint32_t nn = 2 * L - 1;  // nodes; the root (nn - 1) is its own target
@@ -294,6 +318,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         }
         __syncthreads();
     }
+    HPROF(2);  // pointer jumping
     // leaves: code book, and the left-aligned codes, whose order is the preorder of the leaves
     for (uint32_t v = lane; v < 256; v += 64) {
         if (v >= L) {
@@ -338,6 +363,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     }
     __syncthreads();
     DevTable *t = &tabs[b];
+    HPROF(3);  // codes, preorder ranks, tree bits
     uint64_t bits = 0;
     for (uint32_t s = lane; s < 256; s += 64) {
         t->code[s] = s_code[s];
@@ -365,6 +391,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         if (p == 0xffffffffu) e |= kStatusPrimary;
         if (e) atomicOr(status, e);
     }
+    HPROF(4);  // outputs
 }
 
 // One workgroup: record offsets = exclusive scan of (header + payload) sizes.
@@ -462,6 +489,20 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
     }
     BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
                d_status, d_rbase, d_ridx, d_rrank);
+#ifdef BMH_PROF_HUFF
+    {
+        std::vector<uint32_t> h(4096 * 8);
+        BMH_HIP(hipStreamSynchronize(c->stream));
+        BMH_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_hprof), h.size() * 4));
+        double sum[8] = {};
+        const uint32_t m = std::min<uint32_t>(nb, 4096);
+        for (uint32_t w = 0; w < m; ++w)
+            for (int i = 0; i < 8; ++i) sum[i] += h[w * 8 + i];
+        fprintf(stderr, "huff_build phases (mean s_memtime ticks over %u blocks):", m);
+        for (int i = 0; i < 6; ++i) fprintf(stderr, " %.0f", m ? sum[i] / m : 0.0);
+        fprintf(stderr, "\n");
+    }
+#endif
     const uint64_t *d_base = nullptr;
     if (chain && sub > 0) {
         std::unique_lock<std::mutex> lk(chain->m);
