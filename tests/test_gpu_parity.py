@@ -297,6 +297,22 @@ def test_zipf100m_1m_manifest(ctx):
     _blocks_vs_manifest(ctx, man, lambda b: z[b << 20:(b + 1) << 20])
 
 
+@pytest.mark.gpu
+def test_zipf100m_1m_one_batch_four_pipelines(ctx):
+    """Config 3 as one 100 MB batch of 1 MiB blocks: past the run screen with >= 16 blocks, so it
+    runs on four pipelines (the fourth on the D2H stream; capi.cpp stream_count): every record
+    equals the reference manifest and the records land back to back in block order."""
+    man = manifest("zipf100m_1m")
+    z = synth.zipf_text(100_000_000)
+    nb = len(man["blocks"])
+    outs = ctx.encode_blocks([z[b << 20:(b + 1) << 20] for b in range(nb)])
+    agg = hashlib.sha256()
+    for b, o in enumerate(outs):
+        assert hashlib.sha256(o).hexdigest() == man["blocks"][b]["sha256"], b
+        agg.update(o)
+    assert agg.hexdigest() == man["aggregate_sha256"]
+
+
 def test_device_synth_matches_numpy(ctx):
     for off, n in [(0, 1 << 20), (12345, 100001)]:
         d = ctx.alloc(n)
