@@ -73,9 +73,10 @@ _SIGS = {
     "bmh_huffman_build_sized": (C.c_int, [PU64, PU64, U64, C.POINTER(CodeTable)]),
     "bmh_node_ranks": (C.c_int, [U64, U32, C.POINTER(C.c_uint16)]),
     "bmh_payload_bytes": (U64, [C.POINTER(CodeTable), PU64]),
-    "bmh_pack_dev": (C.c_int, [P, P, PU64, U32, C.POINTER(CodeTable), P, PU64]),
+    "bmh_pack_dev": (C.c_int, [P, P, PU64, U32, C.POINTER(CodeTable), P, U64, PU64, PU64]),
     "bmh_encode_blocks_dev": (C.c_int, [P, P, PU64, U32, P, U64, PU64]),
     "bmh_record_bound": (U64, [U64]),
+    "bmh_encode_pipelines": (U32, [P, U64, U32]),
     "bmh_compress_host": (C.c_int, [P, P, U64, U64, P, U64, PU64]),
     "bmh_compress_host_multi": (C.c_int, [C.POINTER(P), U32, P, U64, U64, P, U64, PU64]),
     "bmh_compress_bound": (U64, [U64, U64]),
@@ -90,6 +91,7 @@ _SIGS = {
     "bmh_ctx_reset_stats": (C.c_int, [P]),
     "bmh_ctx_kernel_stats": (C.c_int, [P, P, PU64, C.POINTER(C.c_double), C.c_int]),
     "bmh_synth_splitmix64_dev": (C.c_int, [P, P, U64, U64, U64]),
+    "bmh_synth_zipf_dev": (C.c_int, [P, P, U64, U64]),
     "bmh_check_violations": (C.c_int64, [P, U32]),
 }
 
@@ -235,6 +237,10 @@ class Context:
                "compress_host")
         return n.value
 
+    def pipelines(self, total: int, nblocks: int) -> int:
+        """Pipelines (streams) the library runs a device batch of this shape on."""
+        return int(lib().bmh_encode_pipelines(self.h, total, nblocks))
+
     # ---- measurement
     def set_timing(self, on: bool) -> None:
         _check(lib().bmh_ctx_set_timing(self.h, 1 if on else 0), "set_timing")
@@ -299,6 +305,10 @@ class Context:
 
     def synth_splitmix64(self, d_out, nbytes: int, seed: int = 0, offset: int = 0) -> None:
         _check(lib().bmh_synth_splitmix64_dev(self.h, _dp(d_out), nbytes, seed, offset), "synth")
+
+    def synth_zipf(self, d_out, nbytes: int, offset: int = 0) -> None:
+        """Bytes [offset, offset + nbytes) of the App. D Zipf text stream, generated in HBM."""
+        _check(lib().bmh_synth_zipf_dev(self.h, _dp(d_out), nbytes, offset), "synth")
 
     # ---- host convenience
     def encode_blocks(self, blocks: Sequence) -> list[bytes]:
@@ -471,15 +481,14 @@ def huffman(mtf, ctx: Context | None = None) -> tuple[bytes, CodeTable]:
         freq, first = ctx.histogram_dev(d_m, offs)
         freq, first = freq[0], first[0]
         t = huffman_build(freq, first, a.size)  # the MTF stream has the block's size
-        nbytes = payload_bytes(t, freq)
-        d_out = ctx.alloc(nbytes + 8)
+        cap = (payload_bytes(t, freq) + 3) & ~3  # the pack writes whole 4-byte words
+        d_out = ctx.alloc(cap)
         try:
-            zero = np.zeros(nbytes + 8, dtype=np.uint8)
-            d_out.upload(zero)
             tabs = (CodeTable * 1)(t)
-            po = np.array([0], dtype=np.uint64)
-            _check(lib().bmh_pack_dev(ctx.h, d_m.ptr, _u64p(offs), 1, tabs, d_out.ptr, _u64p(po)), "pack")
-            return d_out.download(nbytes).tobytes(), t
+            nbytes = np.zeros(1, dtype=np.uint64)
+            _check(lib().bmh_pack_dev(ctx.h, d_m.ptr, _u64p(offs), 1, tabs, d_out.ptr, cap, None, _u64p(nbytes)),
+                   "pack")
+            return d_out.download(int(nbytes[0])).tobytes(), t
         finally:
             d_out.free()
     finally:

@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -52,7 +53,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_IN3, WS_OUT3, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_BAND, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_BAND, WS_SYNTH, WS_COUNT_
 };
 
 struct Ctx {
@@ -95,6 +96,10 @@ struct Ctx {
     hipStream_t aux_stream = nullptr;
     Ctx *aux = nullptr;
     int nstreams = 0;  // 0: BMH_STREAMS or the default
+    // size of the batch a sub-pipeline's sub-batch was cut from (0: its own batch): the run
+    // screen is decided on it, so a batch past the screen never sends its sub-batches' run-heavy
+    // blocks to the side stream D, which a fourth pipeline holds (bwt_runs.hip)
+    uint64_t screen_total = 0;
     // BWT: write the suffix array of every slot (needed by rank doubling) instead of only the
     // slots later passes read; set after a batch needed doubling, cleared when one did not
     bool bwt_full_sa = false;
@@ -200,7 +205,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,
                uint32_t *h_first32);
 void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
-                const uint64_t *pay_offs);
+                uint64_t out_cap, const uint64_t *pay_offs, uint64_t *out_bytes);
 // Record offsets of consecutive sub-batches encoded concurrently on several streams: sub-batch
 // s starts where s - 1 ends (a device value), so s waits for s - 1's offset scan.
 struct OffsetChain {
@@ -217,7 +222,8 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
 void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
                     uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist);
 void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_freq32, uint32_t *h_first32);
-void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
+void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);  // synth.hip
+void synth_zipf(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t offset);
 
 // Host Huffman (huffman_host.cpp). n = the block's size: below kBandCeil the tie-break follows
 // the reference's heap history (heap_order.cpp); n = 0 takes the closed-form order.
@@ -233,8 +239,9 @@ struct BandRanks {
     std::vector<uint32_t> off;   // 257 entries
     std::vector<uint16_t> rank;  // node id -> ascending-address rank among the 2L - 1 nodes
 };
-const BandRanks *band_ranks(uint64_t n);
+std::shared_ptr<const BandRanks> band_ranks(uint64_t n);  // LRU-bounded cache (heap_order.cpp)
 void band_ranks_prefetch(const std::vector<uint64_t> &sizes);  // computes the missing ones in parallel
+size_t band_cache_entries();  // sizes currently cached
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank);  // exact ranks (model or heap history)
 uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);
 

@@ -314,7 +314,7 @@ void run_block(Ctx *c, const uint8_t *t, uint32_t n, uint32_t m, uint8_t *L, uin
 void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary)
 {
     const uint32_t nb = bt.nblocks;
-    bool screen = bt.total <= kRunScreenMax;
+    bool screen = (c->screen_total ? c->screen_total : bt.total) <= kRunScreenMax;
     if (screen) {
         screen = false;
         for (uint32_t b = 0; b < nb && !screen; ++b) {

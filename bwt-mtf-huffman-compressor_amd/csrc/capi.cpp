@@ -293,6 +293,8 @@ static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
     return total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
 }
 
+static uint32_t pipelines_for(Ctx *c, uint64_t total, uint32_t nb, int max_pipes);
+
 // The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
 // stream by its own host thread, so that one run's bandwidth-bound kernels overlap another's
 // LDS-bound ones. Records land back to back in block order: each run's offset scan starts
@@ -301,8 +303,7 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
                    uint64_t *rec_offs, int max_pipes)
 {
     const uint32_t nb = bt.nblocks;
-    const int S = (int)std::min<uint32_t>(std::min<uint32_t>((uint32_t)stream_count(c, bt.total, nb), (uint32_t)max_pipes),
-                                          nb / 2);
+    const int S = (int)pipelines_for(c, bt.total, nb, max_pipes);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
         return;
@@ -321,6 +322,7 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     std::vector<Ctx *> cs(S);
     for (int s = 0; s < S; ++s) {
         cs[s] = sub_ctx(c, s);
+        cs[s]->screen_total = bt.total;  // the run screen follows the whole batch (bwt_runs.hip)
         BMH_HIP(hipEventCreateWithFlags(&chain.ev[s], hipEventDisableTiming));
     }
     std::vector<std::vector<uint64_t>> ro(S);
@@ -372,6 +374,14 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     for (int s = 0; s < S; ++s)
         for (uint32_t i = 0; i < cut[s + 1] - cut[s]; ++i) rec_offs[cut[s] + i] = ro[s][i];
     rec_offs[nb] = ro[S - 1][cut[S] - cut[S - 1]];
+}
+
+// Pipelines (streams) encode_blocks runs a device-resident batch of this shape on.
+static uint32_t pipelines_for(Ctx *c, uint64_t total, uint32_t nb, int max_pipes)
+{
+    const uint32_t S = std::min<uint32_t>(std::min<uint32_t>((uint32_t)stream_count(c, total, nb), (uint32_t)max_pipes),
+                                          nb / 2);
+    return S <= 1 ? 1u : S;
 }
 
 static uint64_t max_batch_bytes()
@@ -954,11 +964,17 @@ int bmh_node_ranks(uint64_t n, uint32_t L, uint16_t *rank)
     if (!rank || L == 0 || L > 256) return -1;
     try {
         node_ranks(n, L, rank);
-        const BandRanks *br = band_ranks(n);
+        const auto br = band_ranks(n);
         return br && br->off[L] != kModelOrder ? 1 : 0;
     } catch (...) {
         return -1;
     }
+}
+
+uint32_t bmh_encode_pipelines(bmh_ctx *c, uint64_t total, uint32_t nblocks)
+{
+    if (!c || nblocks == 0) return 0;
+    return pipelines_for(c, total, nblocks, 16);  // as bmh_encode_blocks_dev
 }
 
 uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
@@ -967,13 +983,14 @@ uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
 }
 
 bmh_status bmh_pack_dev(bmh_ctx *c, const uint8_t *d_mtf, const uint64_t *offs, uint32_t nblocks,
-                        const bmh_code_table *tables, uint8_t *d_out, const uint64_t *pay_offs)
+                        const bmh_code_table *tables, uint8_t *d_out, uint64_t out_cap, const uint64_t *pay_offs,
+                        uint64_t *out_bytes)
 {
     API_BEGIN
     use_device(c);
-    if (!d_mtf || !tables || !d_out || !pay_offs) fail(BMH_EINVAL, "null argument");
+    if (!d_mtf || !tables || !d_out) fail(BMH_EINVAL, "null argument");
     Batch bt = make_batch(offs, nblocks);
-    pack_batch(c, d_mtf, bt, tables, d_out, pay_offs);
+    pack_batch(c, d_mtf, bt, tables, d_out, out_cap, pay_offs, out_bytes);
     API_END
 }
 
@@ -1249,6 +1266,15 @@ bmh_status bmh_synth_splitmix64_dev(bmh_ctx *c, uint8_t *d_out, uint64_t nbytes,
     use_device(c);
     if (!d_out) fail(BMH_EINVAL, "null buffer");
     if (nbytes) synth_splitmix64(c, d_out, nbytes, seed, offset);
+    API_END
+}
+
+bmh_status bmh_synth_zipf_dev(bmh_ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t offset)
+{
+    API_BEGIN
+    use_device(c);
+    if (!d_out) fail(BMH_EINVAL, "null buffer");
+    if (nbytes) synth_zipf(c, d_out, nbytes, offset);
     API_END
 }
 

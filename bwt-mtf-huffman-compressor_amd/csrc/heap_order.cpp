@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -503,24 +504,64 @@ std::unique_ptr<BandRanks> compute_band_ranks(uint64_t n)
     return out;
 }
 
+// Process-wide cache of band_ranks per block size, bounded: least recently used
+// sizes are dropped past kBandCacheBytes of rank tables or kBandCacheEntries sizes. Entries are
+// shared_ptr, so a table a caller still holds survives its eviction.
+constexpr size_t kBandCacheBytes = 64u << 20;
+constexpr size_t kBandCacheEntries = 1u << 16;
+struct BandEntry {
+    std::shared_ptr<const BandRanks> r;  // null: the closed form holds for every L
+    uint64_t used;
+    size_t bytes;
+};
 std::mutex g_band_mu;
-std::unordered_map<uint64_t, std::unique_ptr<BandRanks>> g_band;
+std::unordered_map<uint64_t, BandEntry> g_band;
+size_t g_band_bytes = 0;
+uint64_t g_band_clock = 0;
+
+void band_evict_locked()
+{
+    while (g_band.size() > 1 && (g_band_bytes > kBandCacheBytes || g_band.size() > kBandCacheEntries)) {
+        auto lru = g_band.begin();
+        for (auto it = g_band.begin(); it != g_band.end(); ++it)
+            if (it->second.used < lru->second.used) lru = it;
+        g_band_bytes -= lru->second.bytes;
+        g_band.erase(lru);
+    }
+}
 
 }  // namespace
 
-const BandRanks *band_ranks(uint64_t n)
+size_t band_cache_entries()
+{
+    std::lock_guard<std::mutex> lk(g_band_mu);
+    return g_band.size();
+}
+
+std::shared_ptr<const BandRanks> band_ranks(uint64_t n)
 {
     if (n == 0 || n >= kBandCeil) return nullptr;
     {
         std::lock_guard<std::mutex> lk(g_band_mu);
         auto it = g_band.find(n);
-        if (it != g_band.end()) return it->second.get();
+        if (it != g_band.end()) {
+            it->second.used = ++g_band_clock;
+            return it->second.r;
+        }
     }
-    auto r = compute_band_ranks(n);  // outside the lock: other sizes proceed meanwhile
+    std::shared_ptr<const BandRanks> r(compute_band_ranks(n).release());  // outside the lock
     std::lock_guard<std::mutex> lk(g_band_mu);
     auto it = g_band.find(n);
-    if (it == g_band.end()) it = g_band.emplace(n, std::move(r)).first;
-    return it->second.get();
+    if (it == g_band.end()) {
+        const size_t bytes = 64 + (r ? r->off.size() * 4 + r->rank.size() * 2 : 0);
+        it = g_band.emplace(n, BandEntry{std::move(r), ++g_band_clock, bytes}).first;
+        g_band_bytes += bytes;
+        std::shared_ptr<const BandRanks> keep = it->second.r;
+        band_evict_locked();
+        return keep;
+    }
+    it->second.used = ++g_band_clock;
+    return it->second.r;
 }
 
 void band_ranks_prefetch(const std::vector<uint64_t> &sizes)
@@ -539,17 +580,26 @@ void band_ranks_prefetch(const std::vector<uint64_t> &sizes)
     }
     const unsigned nt = std::min<unsigned>((unsigned)todo.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     std::atomic<size_t> next{0};
+    std::mutex emu;
+    std::exception_ptr err;  // the first failure of a worker, rethrown on this thread
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t)
         th.emplace_back([&] {
-            for (size_t i; (i = next.fetch_add(1)) < todo.size();) band_ranks(todo[i]);
+            try {
+                for (size_t i; (i = next.fetch_add(1)) < todo.size();) band_ranks(todo[i]);
+            } catch (...) {
+                std::lock_guard<std::mutex> lk(emu);
+                if (!err) err = std::current_exception();
+                next.store(todo.size());
+            }
         });
     for (auto &x : th) x.join();
+    if (err) std::rethrow_exception(err);
 }
 
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank)
 {
-    const BandRanks *br = band_ranks(n);
+    const auto br = band_ranks(n);
     if (br && L <= 256 && br->off[L] != kModelOrder) {
         memcpy(rank, br->rank.data() + br->off[L], (2 * L - 1) * sizeof(uint16_t));
         return;

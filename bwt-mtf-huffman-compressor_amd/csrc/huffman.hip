@@ -458,7 +458,7 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         }
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t n = bt.offs[b + 1] - bt.offs[b];
-            const BandRanks *br = band_ranks(n);
+            const auto br = band_ranks(n);
             if (!br) continue;
             auto it = seen.find(n);
             if (it == seen.end()) {

@@ -588,6 +588,7 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
     }
     __syncthreads();
     const uint32_t nl = s_nlist;
+    static_assert(kPackChunkSyms == 64 * 64, "k_mtf_first: a wave's 64 lanes x 64 symbols cover one pack chunk");
     for (uint32_t k = w; k < nl; k += kFirstNT / 64) {  // lane l: symbols [64l, 64l + 64) of the chunk
         const uint32_t cm = s_list[k], p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
         const uint32_t e0 = 64 * l;

@@ -59,8 +59,10 @@ __global__ __launch_bounds__(256) void k_pack_bits_hist(const uint16_t *__restri
     if (l == 0) cbits[c] = s;
 }
 
-// grid = nblocks; exclusive scan of the block's chunk bit counts (in place)
-__global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ cfirst, uint64_t *__restrict__ cbits)
+// grid = nblocks; exclusive scan of the block's chunk bit counts (in place); btot (may be null)
+// receives each block's payload bits
+__global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ cfirst, uint64_t *__restrict__ cbits,
+                                                   uint64_t *__restrict__ btot)
 {
     __shared__ uint64_t s_tmp[8];
     const uint32_t c0 = cfirst[blockIdx.x], c1 = cfirst[blockIdx.x + 1];
@@ -73,6 +75,7 @@ __global__ __launch_bounds__(256) void k_pack_scan(const uint32_t *__restrict__ 
         if (i < c1) cbits[i] = carry + ex;
         carry += total;
     }
+    if (btot && threadIdx.x == 0) btot[blockIdx.x] = carry;
 }
 
 // The chunk's image is built in LDS windows of kPackImgWords words: one window whenever the
@@ -289,12 +292,17 @@ void histogram_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint32_t *h_f
     c->sync();
 }
 
-void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
-                    uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist)
+namespace {
+struct PackLayout {
+    const PChunk *chunks;
+    const uint32_t *cfirst;
+    uint32_t nch;
+};
+
+// chunk table: rebuilt and uploaded only when the batch layout changed
+PackLayout pack_layout(Ctx *c, const Batch &bt)
 {
-    if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const uint32_t nb = bt.nblocks;
-    // chunk table: rebuilt and uploaded only when the batch layout changed
     const uint64_t sig = layout_sig(3, bt.offs, 0);
     uint32_t nch;
     if (c->ws_tag[WS_PACK_CHUNKS] == sig) {
@@ -322,23 +330,42 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
         c->ws_tag[WS_PACK_CHUNKS] = sig;
         c->ws_aux[WS_PACK_CHUNKS][0] = nch;
     }
-    uint8_t *d_meta = (uint8_t *)c->ws[WS_PACK_CHUNKS];
-    PChunk *d_chunks = (PChunk *)d_meta;
-    uint32_t *d_cfirst = (uint32_t *)(d_meta + nch * sizeof(PChunk));
-    uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)nch * 8);
-    if (d_chist)
-        BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(nch, 4), 256, 0, d_chist, d_chunks, nch, d_tabs, d_cbits);
-    else
-        BMH_LAUNCH(c, "pack_bits", k_pack_bits, nch, 256, 0, d_mtf, d_chunks, d_tabs, d_cbits);
-    BMH_LAUNCH(c, "pack_scan", k_pack_scan, nb, 256, 0, d_cfirst, d_cbits);
-    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(nch, kPackCPW), 256, 0, d_mtf, d_chunks, nch, d_tabs, d_cbits,
-               d_pay_offs, d_cfirst,
-               (uint32_t *)d_out, d_status);
+    const uint8_t *d_meta = (const uint8_t *)c->ws[WS_PACK_CHUNKS];
+    return PackLayout{(const PChunk *)d_meta, (const uint32_t *)(d_meta + nch * sizeof(PChunk)), nch};
 }
 
-void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
-                const uint64_t *pay_offs)
+// chunk bit counts, then their per-block exclusive scan (block totals into d_btot if non-null)
+uint64_t *pack_bits_scan(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const PackLayout &pl, const DevTable *d_tabs,
+                         const uint16_t *d_chist, uint64_t *d_btot)
 {
+    uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)pl.nch * 8);
+    if (d_chist)
+        BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(pl.nch, 4), 256, 0, d_chist, pl.chunks, pl.nch, d_tabs,
+                   d_cbits);
+    else
+        BMH_LAUNCH(c, "pack_bits", k_pack_bits, pl.nch, 256, 0, d_mtf, pl.chunks, d_tabs, d_cbits);
+    BMH_LAUNCH(c, "pack_scan", k_pack_scan, bt.nblocks, 256, 0, pl.cfirst, d_cbits, d_btot);
+    return d_cbits;
+}
+}  // namespace
+
+void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTable *d_tabs, const uint64_t *d_pay_offs,
+                    uint8_t *d_out, const uint32_t *d_status, const uint16_t *d_chist)
+{
+    if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
+    const PackLayout pl = pack_layout(c, bt);
+    const uint64_t *d_cbits = pack_bits_scan(c, d_mtf, bt, pl, d_tabs, d_chist, nullptr);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, kPackCPW), 256, 0, d_mtf, pl.chunks, pl.nch, d_tabs, d_cbits,
+               d_pay_offs, pl.cfirst, (uint32_t *)d_out, d_status);
+}
+
+// The standalone stage (bmh_pack_dev): payload sizes first (one wait), checked against the
+// caller's buffer, then the write. The write touches whole 4-byte words (edge words under a mask),
+// so every payload's word-rounded extent must lie inside [d_out, d_out + out_cap).
+void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,
+                uint64_t out_cap, const uint64_t *pay_offs, uint64_t *out_bytes)
+{
+    if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const uint32_t nb = bt.nblocks;
     std::vector<DevTable> ht(nb);
     for (uint32_t b = 0; b < nb; ++b) {
@@ -349,45 +376,37 @@ void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_ta
     }
     DevTable *d_tab = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
     uint64_t *d_pay = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 1) * 8 + 64);
+    uint64_t *d_btot = d_pay + nb;
     c->h2d(d_tab, ht.data(), nb * sizeof(DevTable));
-    c->h2d(d_pay, pay_offs, nb * 8);
-    pack_batch_dev(c, d_mtf, bt, d_tab, d_pay, d_out, nullptr, nullptr);
+    const PackLayout pl = pack_layout(c, bt);
+    const uint64_t *d_cbits = pack_bits_scan(c, d_mtf, bt, pl, d_tab, nullptr, d_btot);
+    std::vector<uint64_t> bits(nb), bytes(nb), po(nb);
+    c->d2h(bits.data(), d_btot, nb * 8);
     c->sync();
-}
-
-// ---------------------------------------------------------------- synthetic input (App. D)
-namespace {
-__device__ __forceinline__ uint64_t splitmix_word(uint64_t seed, uint64_t k)
-{
-    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-__global__ void k_splitmix(uint8_t *__restrict__ out, uint64_t nbytes, uint64_t seed, uint64_t offset)
-{
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t i0 = t * 8;
-    if (i0 >= nbytes) return;
-    const uint64_t g = offset + i0;
-    const uint64_t w = g >> 3;
-    const uint32_t s = (uint32_t)(g & 7u);
-    const uint64_t z0 = splitmix_word(seed, w);
-    uint64_t v = z0 >> (8 * s);
-    if (s) v |= splitmix_word(seed, w + 1) << (64 - 8 * s);
-    if (i0 + 8 <= nbytes && (((uintptr_t)(out + i0)) & 7u) == 0) {
-        *(uint64_t *)(out + i0) = v;
-    } else {
-        for (uint32_t j = 0; j < 8 && i0 + j < nbytes; ++j) out[i0 + j] = (uint8_t)(v >> (8 * j));
+    uint64_t next = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        bytes[b] = std::max<uint64_t>(1, (bits[b] + 7) / 8);  // encode_with_huffman's one zero byte, main.cpp:162
+        po[b] = pay_offs ? pay_offs[b] : next;
+        next = po[b] + bytes[b];
+        if (po[b] > out_cap || bytes[b] > out_cap - po[b] || ((po[b] + bytes[b] + 3) & ~(uint64_t)3) > out_cap)
+            fail(BMH_ERANGE, "pack: payload of block " + std::to_string(b) + " (" + std::to_string(bytes[b]) +
+                                 " B at " + std::to_string(po[b]) + ") does not fit out_cap " + std::to_string(out_cap) +
+                                 " (whole 4-byte words)");
     }
-}
-}  // namespace
-
-void synth_splitmix64(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset)
-{
-    const uint64_t threads = (nbytes + 7) / 8;
-    BMH_LAUNCH(c, "synth_splitmix64", k_splitmix, (uint32_t)((threads + 255) / 256), 256, 0, d_out, nbytes, seed, offset);
+    if (pay_offs) {  // payloads must not overlap (edge words are shared under a mask, bytes are not)
+        std::vector<uint32_t> ord(nb);
+        for (uint32_t b = 0; b < nb; ++b) ord[b] = b;
+        std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return po[x] < po[y]; });
+        for (uint32_t i = 1; i < nb; ++i)
+            if (po[ord[i - 1]] + bytes[ord[i - 1]] > po[ord[i]])
+                fail(BMH_EINVAL, "pack: payloads of blocks " + std::to_string(ord[i - 1]) + " and " +
+                                     std::to_string(ord[i]) + " overlap");
+    }
+    c->h2d(d_pay, po.data(), nb * 8);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, kPackCPW), 256, 0, d_mtf, pl.chunks, pl.nch, d_tab, d_cbits,
+               d_pay, pl.cfirst, (uint32_t *)d_out, nullptr);
     c->sync();
+    if (out_bytes) memcpy(out_bytes, bytes.data(), nb * 8);
 }
 
 }  // namespace bmh

@@ -108,17 +108,26 @@ int bmh_node_ranks(uint64_t n, uint32_t L, uint16_t *rank);
 /* Payload bytes encode_with_huffman (main.cpp:158-172) emits: max(1, ceil(sum freq*len / 8)). */
 uint64_t bmh_payload_bytes(const bmh_code_table *table, const uint64_t freq[256]);
 
-/* Replaces encode_with_huffman() (main.cpp:158-172): MSB-first concatenation of code words.
- * tables[b] is block b's table; block b's payload is written at d_out + pay_offs[b]
- * (pay_offs: host array, nblocks entries; the caller sizes each with bmh_payload_bytes). */
+/* Replaces encode_with_huffman() (main.cpp:158-172): MSB-first concatenation of code words,
+ * max(1, ceil(bits / 8)) bytes per block. tables[b] is block b's table; block b's payload is
+ * written at d_out + pay_offs[b] (pay_offs: host array of nblocks entries, or NULL for payloads
+ * back to back from d_out). d_out must be 4-byte aligned: the pack writes whole 4-byte words
+ * (bytes of an edge word outside the payload are preserved), so each payload's extent rounded up
+ * to a 4-byte boundary must fit in out_cap, else BMH_ERANGE and nothing is written; overlapping
+ * payloads are BMH_EINVAL. out_bytes (host, nblocks entries, may be NULL) receives each
+ * payload's byte count (= bmh_payload_bytes). */
 bmh_status bmh_pack_dev(bmh_ctx *ctx, const uint8_t *d_mtf, const uint64_t *offs, uint32_t nblocks,
-                        const bmh_code_table *tables, uint8_t *d_out, const uint64_t *pay_offs);
+                        const bmh_code_table *tables, uint8_t *d_out, uint64_t out_cap, const uint64_t *pay_offs,
+                        uint64_t *out_bytes);
 
 /* Whole encode (compress(), main.cpp:300-325, minus file I/O): one reference record per
  * block, [u64 primary][u64 n][u64 tree_len][tree][payload] (io_utilities.h:7-27), written
  * back to back at d_out. h_rec_offs (nblocks+1 entries) receives the record offsets. */
 bmh_status bmh_encode_blocks_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
                                  uint8_t *d_out, uint64_t out_cap, uint64_t *h_rec_offs);
+/* Pipelines (HIP streams, each driven by its own host thread) bmh_encode_blocks_dev runs a batch
+ * of nblocks blocks totalling `total` bytes on (the library's rule; BMH_STREAMS overrides). */
+uint32_t bmh_encode_pipelines(bmh_ctx *ctx, uint64_t total, uint32_t nblocks);
 /* Capacity sufficient for one record of an n-byte block. */
 uint64_t bmh_record_bound(uint64_t n);
 
@@ -177,6 +186,9 @@ int64_t bmh_check_violations(bmh_ctx *ctx, uint32_t kind);
 /* Synthetic input: bytes [offset, offset+nbytes) of the little-endian
  * splitmix64(seed) stream, generated on the device. */
 bmh_status bmh_synth_splitmix64_dev(bmh_ctx *ctx, uint8_t *d_out, uint64_t nbytes, uint64_t seed, uint64_t offset);
+/* Synthetic input: bytes [offset, offset+nbytes) of the integer-Zipf text
+ * stream (configs 3 and 5), generated on the device. */
+bmh_status bmh_synth_zipf_dev(bmh_ctx *ctx, uint8_t *d_out, uint64_t nbytes, uint64_t offset);
 
 #ifdef __cplusplus
 }

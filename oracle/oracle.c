@@ -408,3 +408,71 @@ int64_t orc_decode_record(const uint8_t *rec, size_t len, uint8_t *out, size_t c
     free(Lb);
     return ret;
 }
+
+/* ---- synthetic Zipf text (not reference code: the config-5 input) ----
+ * A sequential restatement of the App. D generator, used as the checker of the device generator
+ * (bmh_synth_zipf_dev) and to stream the 8 GiB config-5 input through the reference when the
+ * golden manifest is made (tests/golden/make_golden.py). */
+#define ORC_ZIPF_VOCAB 8192
+struct orc_zipf {
+    uint64_t cdf[ORC_ZIPF_VOCAB];
+    uint8_t word[ORC_ZIPF_VOCAB][12]; /* letters + ' ' */
+    uint8_t wlen[ORC_ZIPF_VOCAB];     /* including the space */
+    uint64_t tok;                     /* tokens drawn so far from splitmix64(seed 2) */
+    uint8_t pend[12];                 /* tail of a token cut at the previous call's end */
+    int npend, ipend;
+};
+
+static uint64_t sm64_at(uint64_t seed, uint64_t k) /* k-th output, k >= 1 */
+{
+    uint64_t z = seed + k * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+size_t orc_zipf_state_size(void) { return sizeof(struct orc_zipf); }
+
+void orc_zipf_init(struct orc_zipf *z)
+{
+    uint64_t k = 0, acc = 0;
+    for (int w = 0; w < ORC_ZIPF_VOCAB; ++w) {
+        uint64_t r = sm64_at(1, ++k);
+        int ln = 2 + (int)(r % 9);
+        for (int i = 0; i < ln; ++i) z->word[w][i] = (uint8_t)('a' + sm64_at(1, ++k) % 26);
+        z->word[w][ln] = ' ';
+        z->wlen[w] = (uint8_t)(ln + 1);
+        acc += (1ull << 32) / (uint64_t)(w + 1);
+        z->cdf[w] = acc;
+    }
+    z->tok = 0;
+    z->npend = z->ipend = 0;
+}
+
+/* Next n bytes of the stream. */
+void orc_zipf_fill(struct orc_zipf *z, uint8_t *out, size_t n)
+{
+    size_t o = 0;
+    const uint64_t T = z->cdf[ORC_ZIPF_VOCAB - 1];
+    while (o < n && z->ipend < z->npend) out[o++] = z->pend[z->ipend++];
+    while (o < n) {
+        uint64_t x = sm64_at(2, ++z->tok) % T;
+        int lo = 0, hi = ORC_ZIPF_VOCAB - 1; /* first k with cdf[k] > x */
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (z->cdf[mid] > x) hi = mid; else lo = mid + 1;
+        }
+        int ln = z->wlen[lo];
+        if (o + (size_t)ln <= n) {
+            memcpy(out + o, z->word[lo], (size_t)ln);
+            o += (size_t)ln;
+        } else {
+            int take = (int)(n - o);
+            memcpy(out + o, z->word[lo], (size_t)take);
+            o = n;
+            memcpy(z->pend, z->word[lo] + take, (size_t)(ln - take));
+            z->npend = ln - take;
+            z->ipend = 0;
+        }
+    }
+}

@@ -47,6 +47,13 @@ int64_t orc_decode_record(const uint8_t *rec, size_t len, uint8_t *out, size_t c
 /* Huffman-decode only (main.cpp:259-281): record -> MTF stream. Returns n or -1. */
 int64_t orc_decode_to_mtf(const uint8_t *rec, size_t len, uint8_t *mtf_out, size_t cap);
 
+/* SURVEY App. D integer-Zipf text stream (config 5's input), generated sequentially:
+ * state of orc_zipf_state_size() bytes, orc_zipf_init, then orc_zipf_fill for the next n bytes. */
+struct orc_zipf;
+size_t orc_zipf_state_size(void);
+void orc_zipf_init(struct orc_zipf *z);
+void orc_zipf_fill(struct orc_zipf *z, uint8_t *out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

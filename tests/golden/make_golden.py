@@ -60,21 +60,30 @@ def entry(rec: bytes) -> dict:
 
 
 def blocks_manifest(name: str, gen, nblocks: int, jobs: int, tmpdir: str, note: str) -> None:
+    """gen(b) -> block b's bytes. It is called in block order from this thread (so a sequential
+    generator works); at most 2 * jobs blocks are held in memory at a time."""
     t0 = time.time()
 
-    def one(b):
-        rec, _ = run_ref(gen(b), tmpdir, f"{name}_{b}")
-        return b, rec
+    def one(b, data):
+        rec, _ = run_ref(data, tmpdir, f"{name}_{b}")
+        return rec
 
-    recs = [None] * nblocks
-    with cf.ThreadPoolExecutor(jobs) as ex:
-        for b, rec in ex.map(one, range(nblocks)):
-            recs[b] = rec
+    ents = [None] * nblocks
     agg = hashlib.sha256()
-    for r in recs:
-        agg.update(r)
-    man = {"config": name, "note": note, "blocks": [entry(r) for r in recs],
-           "total_record_bytes": sum(len(r) for r in recs), "aggregate_sha256": agg.hexdigest(),
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        pending = {}
+        nxt = 0  # next block to fold into the aggregate (records are hashed in block order)
+        for b in range(nblocks):
+            pending[b] = ex.submit(one, b, gen(b))
+            while len(pending) >= 2 * jobs or (b == nblocks - 1 and pending):
+                rec = pending.pop(nxt).result()
+                ents[nxt] = entry(rec)
+                agg.update(rec)
+                nxt += 1
+                if nxt % 32 == 0:
+                    print(f"  {name}: {nxt}/{nblocks} blocks, {time.time() - t0:.0f} s", flush=True)
+    man = {"config": name, "note": note, "blocks": ents,
+           "total_record_bytes": sum(e["record_len"] for e in ents), "aggregate_sha256": agg.hexdigest(),
            "generated_by": "oracle/_ref/ref_COMPRESS (reference main.cpp, g++ -O3)",
            "ref_wall_s": round(time.time() - t0, 2), "ref_procs": jobs}
     os.makedirs(os.path.join(HERE, "manifests"), exist_ok=True)
@@ -99,6 +108,7 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--jobs", type=int, default=8)
     ap.add_argument("--skip-random", action="store_true")
+    ap.add_argument("--zipf-blocks", type=int, default=512)
     ap.add_argument("--only", default="")
     a = ap.parse_args()
     if not os.path.exists(REF):
@@ -142,9 +152,15 @@ def main() -> None:
             blocks_manifest("calgary_256k", lambda b: blocks[b], len(blocks), a.jobs, tmp,
                             "Calgary corpus, file order (main.cpp:418), each file cut into 256 KiB blocks")
         if not only or "zipf_16m" in only:
-            z = synth.zipf_text(8 * (16 << 20)).tobytes()
-            blocks_manifest("zipf_16m", lambda b: z[b * (16 << 20):(b + 1) * (16 << 20)], 8, a.jobs, tmp,
-                            "first 8 x 16 MiB blocks of the App. D Zipf text stream")
+            # config 5: the whole 8 GiB App. D stream, 512 x 16 MiB blocks, generated block by
+            # block by the oracle's sequential C generator (checked against the App. D sha256 of
+            # the first 16 MiB and against bmh.synth.zipf_text in tests/test_oracle.py)
+            sys.path.insert(0, os.path.dirname(HERE))
+            from oracle_ffi import Oracle, ZipfStream
+            zs = ZipfStream(Oracle())
+            blocks_manifest("zipf_16m", lambda b: zs.read(16 << 20).tobytes(), a.zipf_blocks, a.jobs, tmp,
+                            f"config 5: the App. D Zipf text stream cut into 16 MiB blocks, blocks "
+                            f"0..{a.zipf_blocks - 1} ({a.zipf_blocks * 16 >> 10} GiB)")
         if not only or "zipf100m_1m" in only:
             z = synth.zipf_text(100_000_000).tobytes()
             nb = (len(z) + (1 << 20) - 1) >> 20

@@ -45,6 +45,9 @@ class Oracle:
         L.orc_decode_to_mtf.restype = C.c_int64
         L.orc_huffman_build.argtypes = [u8p, u8p, u8p, u8p, u8p, C.c_size_t]
         L.orc_huffman_build.restype = C.c_int
+        L.orc_zipf_state_size.restype = C.c_size_t
+        L.orc_zipf_init.argtypes = [u8p]
+        L.orc_zipf_fill.argtypes = [u8p, u8p, C.c_size_t]
         self.L = L
 
     @staticmethod
@@ -120,6 +123,20 @@ class Oracle:
         if r < 0:
             raise ValueError("oracle decode failed")
         return out[:r].tobytes()
+
+
+class ZipfStream:
+    """SURVEY App. D Zipf text, read sequentially from the oracle's C generator."""
+
+    def __init__(self, oracle: "Oracle"):
+        self.L = oracle.L
+        self.st = C.create_string_buffer(self.L.orc_zipf_state_size())
+        self.L.orc_zipf_init(C.addressof(self.st))
+
+    def read(self, n: int) -> np.ndarray:
+        out = np.empty(n, np.uint8)
+        self.L.orc_zipf_fill(C.addressof(self.st), out.ctypes.data, n)
+        return out
 
 
 def golden_calgary():

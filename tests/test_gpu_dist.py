@@ -37,8 +37,9 @@ def test_world2_bench_on_gpu(scaling):
            "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling]
     if scaling == "weak":  # 64 blocks per rank, every leg of the default line
         cmd += ["--bytes-per-gpu", str(256 << 20), "--decode-steps", "1", "--pcie-steps", "1", "--calgary-steps", "1"]
-    else:
-        cmd += ["--decode-steps", "0", "--pcie-steps", "0", "--calgary-steps", "0"]
+    else:  # config 4 as written (1 GiB dealt over the ranks) + the 1 GiB-per-GPU leg, here 256 MiB
+        cmd += ["--decode-steps", "0", "--pcie-steps", "0", "--calgary-steps", "0", "--bytes-per-gpu",
+                str(256 << 20), "--weak-steps", "1"]
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.strip().splitlines() if x.startswith("{")][-1])
@@ -47,6 +48,14 @@ def test_world2_bench_on_gpu(scaling):
     nblk = 128 if scaling == "weak" else 256  # blocks over both ranks
     assert line["parity"] == f"{nblk}/{nblk} records byte-identical to the reference manifest", line["parity"]
     assert line["cpu_baseline"] is None  # N > 1: the CPU baseline is an N = 1 leg
+    # the pipelines the library really runs for the rank's batch (capi.cpp stream_count)
+    assert line["config"]["streams_per_gpu"] == 4
+    if scaling == "strong":
+        w = line["weak_scaling"]
+        assert w["bytes_per_gpu"] == 256 << 20 and w["value"] > 0 and w["streams_per_gpu"] == 4
+        assert w["parity"] == "128/128 records byte-identical to the reference manifest", w
+    else:
+        assert line["weak_scaling"] is None
     if scaling == "weak":
         assert line["decode"]["roundtrip_bit_exact"]
         assert line["pcie_inclusive"]["records_equal_device_encode"]

@@ -216,15 +216,43 @@ def test_pack_dev_multiblock_windows(ctx):
     d_out = ctx.alloc(total)
     d_out.upload(np.full(total, 0xA5, np.uint8))
     ct = (bmh.CodeTable * 3)(*tabs)
-    bmh._check(bmh.lib().bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, bmh._u64p(po)), "pack")
+    nbytes = np.zeros(3, np.uint64)
+    bmh._check(bmh.lib().bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, total, bmh._u64p(po),
+                                      bmh._u64p(nbytes)), "pack")
     out = d_out.download(total).tobytes()
-    d_m.free()
-    d_out.free()
+    assert [int(x) for x in nbytes] == [len(r) for r in refs]
     for b in range(3):
         assert out[int(po[b]):int(po[b]) + len(refs[b])] == refs[b], f"block {b}"
     # bytes outside the payloads are untouched (edge words are updated under a mask)
     assert out[:3] == b"\xa5" * 3
     assert out[int(po[0]) + len(refs[0]):int(po[1])] == b"\xa5"
+
+    # pay_offs = NULL: payloads back to back from d_out
+    packed = sum(len(r) for r in refs)
+    d_out.upload(np.full(total, 0xA5, np.uint8))
+    bmh._check(bmh.lib().bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, (packed + 3) & ~3, None,
+                                      None), "pack back to back")
+    assert d_out.download(packed).tobytes() == b"".join(refs)
+
+    # the boundary checks its buffer: a payload past out_cap (also by the
+    # word-rounded end) is BMH_ERANGE and nothing is written; overlapping payloads are BMH_EINVAL
+    d_out.upload(np.full(total, 0xA5, np.uint8))
+    L = bmh.lib()
+    end2 = int(po[2]) + len(refs[2])
+    word_end = (end2 + 3) & ~3
+    for cap in (end2 - 1, word_end - 1, 0):
+        st = L.bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, cap, bmh._u64p(po), None)
+        assert st == bmh.BMH_ERANGE, cap
+    po_bad = po.copy()
+    po_bad[1] = po[0] + len(refs[0]) - 1
+    st = L.bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, total, bmh._u64p(po_bad), None)
+    assert st == bmh.BMH_EINVAL
+    assert d_out.download(total).tobytes() == b"\xa5" * total
+    # the context stays usable
+    bmh._check(L.bmh_pack_dev(ctx.h, d_m.ptr, bmh._u64p(offs), 3, ct, d_out.ptr, total, bmh._u64p(po), None), "pack")
+    assert d_out.download(total).tobytes()[int(po[1]):int(po[1]) + len(refs[1])] == refs[1]
+    d_m.free()
+    d_out.free()
 
 
 def test_mtf_long_block_chunked(ctx, oracle):
@@ -286,9 +314,77 @@ def test_random_1g_4m_manifest(ctx):
 
 
 def test_zipf_16m_manifest(ctx):
-    man = manifest("zipf_16m")
+    """Config 5's first 8 blocks as one device batch (the full 512 are streamed below)."""
+    man = dict(manifest("zipf_16m"))
+    man["blocks"] = man["blocks"][:8]
     z = synth.zipf_text(8 * (16 << 20))
-    _blocks_vs_manifest(ctx, man, lambda b: z[b * (16 << 20):(b + 1) * (16 << 20)])
+    outs = ctx.encode_blocks([z[b * (16 << 20):(b + 1) * (16 << 20)] for b in range(8)])
+    for b, o in enumerate(outs):
+        assert hashlib.sha256(o).hexdigest() == man["blocks"][b]["sha256"], b
+
+
+def test_device_zipf_matches_oracle(ctx, oracle):
+    """bmh_synth_zipf_dev (synth.hip) against SURVEY App. D's sha256 of the first 16 MiB and the
+    oracle's sequential generator at windows that start and end inside tokens, inside a round and
+    across the 2^26-token round boundary (~470 MB)."""
+    from oracle_ffi import ZipfStream
+    d = ctx.alloc(16 << 20)
+    ctx.synth_zipf(d, 16 << 20, 0)
+    assert hashlib.sha256(d.download().tobytes()).hexdigest() == \
+        "b8b5a2980d7a3c0ec97b8eafa08eaf2423aa1696be1fb47b191566c737d2b889"
+    zs = ZipfStream(oracle)
+    pos = 0
+    for off, n in [(3, 1), (12345, 1000001), (469_999_000, 2_000_000), (512 << 20, 4096)]:
+        zs.read(off - pos)
+        ref = zs.read(n)
+        pos = off + n
+        ctx.synth_zipf(d, n, off)
+        assert d.download(n).tobytes() == ref.tobytes(), (off, n)
+
+
+@pytest.mark.timeout(900)
+def test_config5_8g_stream_manifest(ctx):
+    """BASELINE config 5 on its true input: the 8 GiB App. D Zipf stream (generated in HBM by
+    bmh_synth_zipf_dev, copied to pageable host memory), encoded in 16 MiB blocks by
+    bmh_compress_host (H2D / encode / D2H overlapped on side streams). All 512 records equal the
+    reference's (manifest made by oracle/_ref/ref_COMPRESS, tests/golden/make_golden.py), the
+    aggregate sha256 too, and sampled records decode back on the GPU."""
+    L = bmh.lib()
+    man = manifest("zipf_16m")
+    nb = len(man["blocks"])
+    assert nb == 512
+    bs = 16 << 20
+    n = nb * bs
+    data = np.empty(n, np.uint8)
+    piece = 1 << 30
+    d = ctx.alloc(piece)
+    for off in range(0, n, piece):
+        ctx.synth_zipf(d, piece, off)
+        bmh._check(L.bmh_memcpy_d2h(ctx.h, bmh._ptr(data[off:off + piece]), d.ptr, piece), "d2h")
+    d.free()
+    assert hashlib.sha256(data[:bs]).hexdigest() == \
+        "b8b5a2980d7a3c0ec97b8eafa08eaf2423aa1696be1fb47b191566c737d2b889"
+    out = np.empty(int(L.bmh_compress_bound(n, bs)), np.uint8)
+    olen = ctx.compress_into(data, bs, out)
+    assert bmh.is_container(out[:olen])
+    hdr = out[:32].view("<u8")
+    assert int(hdr[1]) == bs and int(hdr[2]) == nb and int(hdr[3]) == n
+    rlen = out[32:32 + 8 * nb].view("<u8").astype(np.int64)
+    assert [int(x) for x in rlen] == [b["record_len"] for b in man["blocks"]]
+    pos = 32 + 8 * nb
+    agg = hashlib.sha256()
+    bad = []
+    for b in range(nb):
+        r = out[pos:pos + int(rlen[b])]
+        if hashlib.sha256(r).hexdigest() != man["blocks"][b]["sha256"]:
+            bad.append(b)
+        agg.update(r)
+        if b in (0, 1, 255, 511):
+            assert ctx.decompress_bytes(r) == data[b * bs:(b + 1) * bs].tobytes(), b
+        pos += int(rlen[b])
+    assert pos == olen
+    assert not bad, f"{len(bad)} records differ from the reference, first {bad[:8]}"
+    assert agg.hexdigest() == man["aggregate_sha256"]
 
 
 def test_zipf100m_1m_manifest(ctx):

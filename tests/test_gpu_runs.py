@@ -122,3 +122,29 @@ def test_calgary_pic_takes_run_path(ctx):
     ctx.set_timing(False)
     assert rec == gold
     assert "bwt_run_sort" in st and "bwt_g1_scatter" not in st, sorted(st)
+
+
+def _np_runs(seed: int, n: int, alphabet: int, mean_run: float) -> np.ndarray:
+    """Geometric runs (consecutive runs differ) built with numpy, for multi-MiB blocks."""
+    rng = np.random.default_rng(seed)
+    k = int(n / mean_run * 1.5) + 64
+    lens = rng.geometric(1.0 / mean_run, k)
+    vals = np.cumsum(rng.integers(1, alphabet, k)) % alphabet
+    return np.repeat(vals.astype(np.uint8), lens)[:n]
+
+
+def test_run_heavy_blocks_in_four_pipeline_batch(ctx, oracle):
+    """a batch past the run screen (> 64 MiB) of >= 16 blocks runs on four pipelines,
+    the fourth on stream D, the run path's side stream. The screen is decided on the whole batch
+    (Ctx::screen_total), so its run-heavy blocks (1-4 MiB, <= n/4 runs) stay on the rotation sorter
+    and never queue behind pipeline 3. Every record equals the same block encoded alone (where the
+    screen sends it down the run path), and one block equals the oracle."""
+    sizes = [(4 << 20) - 3 * b * 7919 if b % 3 else (1 << 20) + b * 4099 for b in range(20)]
+    blocks = [_np_runs(100 + b, n, (3, 17, 200)[b % 3], (6.0, 12.0, 40.0)[b % 3]) for b, n in enumerate(sizes)]
+    assert sum(sizes) > 64 << 20 and len(blocks) >= 16
+    for b in blocks:  # run-heavy by the screen's rule (runs <= n / 4)
+        assert int(np.count_nonzero(b != np.roll(b, 1))) * 4 <= b.size
+    recs = ctx.encode_blocks(blocks)
+    for i, blk in enumerate(blocks):
+        assert recs[i] == ctx.encode_blocks([blk])[0], i
+    assert recs[0] == oracle.encode(blocks[0])

@@ -111,6 +111,22 @@ def test_synth_hashes():
         "b8b5a2980d7a3c0ec97b8eafa08eaf2423aa1696be1fb47b191566c737d2b889"
 
 
+def test_oracle_zipf_stream_pinned(oracle):
+    """The oracle's sequential App. D Zipf generator (config 5's input, used to make the 512-block
+    zipf_16m manifest): App. D's sha256 of the first 16 MiB, the numpy generator's bytes, and
+    reads of any length continue the same stream (tokens cut across reads)."""
+    from oracle_ffi import ZipfStream
+    z = ZipfStream(oracle)
+    parts = [z.read(n) for n in (1, 5, 1000003, 17, (16 << 20) - 1000026)]
+    a = np.concatenate(parts)
+    assert hashlib.sha256(a.tobytes()).hexdigest() == \
+        "b8b5a2980d7a3c0ec97b8eafa08eaf2423aa1696be1fb47b191566c737d2b889"
+    assert (a[: 1 << 21] == synth.zipf_text(1 << 21)).all()
+    man = manifest("zipf_16m")
+    assert len(man["blocks"]) == 512 and all(b["n"] == 16 << 20 for b in man["blocks"])
+    assert man["blocks"][0]["primary"] == 6326714 and man["blocks"][0]["record_len"] == 5038328
+
+
 def test_full_pipeline_fixture_sizes_and_decode(oracle):
     """The reference's FULL_PIPELINE records (tests/golden/full_pipeline, make_full_pipeline.py):
     same sizes and headers as its standalone COMPRESS records, tree bytes may differ (heap

@@ -2,10 +2,10 @@
 """BASELINE config 5 at full size on one GPU: 8 GiB of Zipf text in 16 MiB blocks
 (512 blocks), streamed from host memory by bmh_compress_host (H2D / encode / D2H overlapped) and,
 when asked, by bmh_compress_host_multi over several contexts (the multi-GPU deal; on a 1-GPU box
-the contexts share device 0). The text is the stream's first 256 MiB repeated (the App. D
-generator is sequential Python, ~7 min for 8 GiB), so blocks 0-15 are the true stream's: blocks
-0-7 are checked record for record against the reference's manifest (zipf_16m). Every block is
-round-tripped by the GPU decoder (bmh_decompress_dev) and compared with the input.
+the contexts share device 0). The text is the true App. D stream, generated in HBM by
+bmh_synth_zipf_dev and copied to pageable host memory; every record is checked against the
+reference's 512-block manifest (zipf_16m, tests/golden/make_golden.py) and the whole container
+is round-tripped by the GPU decoder (bmh_decompress_dev).
 usage: python tools/config5_run.py [--gib 8] [--contexts 1]"""
 import argparse
 import ctypes as C
@@ -20,7 +20,6 @@ import numpy as np
 REPO = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(REPO, "bwt-mtf-huffman-compressor_amd"))
 import bmh  # noqa: E402
-from bmh import synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=int, default=8)
@@ -28,11 +27,18 @@ ap.add_argument("--contexts", type=int, default=1)
 a = ap.parse_args()
 n = a.gib << 30
 bs = 16 << 20
-t0 = time.perf_counter()
-data = np.resize(synth.zipf_text(256 << 20), n)
-gen_s = time.perf_counter() - t0
 L = bmh.lib()
 ctxs = [bmh.Context(0) for _ in range(a.contexts)]
+t0 = time.perf_counter()
+data = np.empty(n, dtype=np.uint8)
+piece = 1 << 30
+d = ctxs[0].alloc(piece)
+for off in range(0, n, piece):
+    m = min(piece, n - off)
+    ctxs[0].synth_zipf(d, m, off)
+    bmh._check(L.bmh_memcpy_d2h(ctxs[0].h, bmh._ptr(data[off:off + m]), d.ptr, m), "d2h")
+d.free()
+gen_s = time.perf_counter() - t0
 cap = int(L.bmh_compress_bound(n, bs))
 out = np.empty(cap, dtype=np.uint8)
 olen = C.c_uint64()
@@ -57,7 +63,8 @@ dt = time.perf_counter() - t1
 rec = out[: olen.value]
 recs = bmh.container_records(rec)
 man = json.load(open(os.path.join(REPO, "tests", "golden", "manifests", "zipf_16m.json")))
-ref_ok = all(hashlib.sha256(recs[i]).hexdigest() == b["sha256"] for i, b in enumerate(man["blocks"]))
+nchk = min(len(recs), len(man["blocks"]))
+ref_eq = sum(hashlib.sha256(recs[i]).hexdigest() == man["blocks"][i]["sha256"] for i in range(nchk))
 back = np.empty(n, dtype=np.uint8)
 nout = C.c_uint64()
 t2 = time.perf_counter()
@@ -68,5 +75,5 @@ ok = st == 0 and nout.value == n and np.array_equal(back, data)
 print(json.dumps({"config": "5: Zipf text, 16 MiB blocks, host buffers in and out", "GiB": a.gib,
                   "blocks": len(recs), "contexts": a.contexts, "ms": round(dt * 1e3, 1),
                   "MBps_pcie_inclusive": round(n / dt / 1e6, 1), "ratio": round(olen.value / n, 6),
-                  "blocks_0_7_equal_reference_manifest": bool(ref_ok), "roundtrip_bit_exact": bool(ok),
+                  "records_equal_reference_manifest": f"{ref_eq}/{nchk}", "roundtrip_bit_exact": bool(ok),
                   "decode_s": round(dec_s, 2), "gen_s": round(gen_s, 1)}))
