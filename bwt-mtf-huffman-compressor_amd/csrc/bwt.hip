@@ -37,40 +37,17 @@ namespace {
 
 // ---------------------------------------------------------------------------- constants
 constexpr uint32_t kG1Chunk = 16384;            // positions per global-pass workgroup (LDS-staged)
-// The persistent LDS-DMA global pass (k_g1_scatter_p, BMH_G1P_PER_CU workgroups per CU) is a
-// build option: measured 3.59 (1 per CU) / 3.85 ms (2 per CU) per GiB against 3.28 ms for one
-// workgroup per chunk.
-#ifndef BMH_SCATTER_P
-#define BMH_SCATTER_P 0
-#endif
-#ifndef BMH_G1P_PER_CU
-#define BMH_G1P_PER_CU 1
-#endif
-#ifndef BMH_G1_BITS
-#define BMH_G1_BITS 10
-#endif
-constexpr uint32_t kG1Bits = BMH_G1_BITS;       // global-pass digit: first byte + (kG1Bits - 8) bits
+constexpr uint32_t kG1Bits = 10;                // global-pass digit: first byte + 2 bits
 constexpr uint32_t kG1Bins = 1u << kG1Bits;
 constexpr uint32_t kSegDigit = 12;              // LDS digit of the finish passes
 constexpr uint32_t kSegDigits1 = 1u << kSegDigit;
-// finish workgroup shapes: dense (global-pass buckets), list small, list big
-// Dense finish of the global pass's buckets: 10-bit pass -> k_finish_dense (<= 4608 rotations,
-// 12-bit digit, R-bit rests); 9-bit pass -> k_finish_wide (<= 9216, 13-bit digit, 16-bit rests).
-// List segments over kFinCap take the counting-sort finish up to kSegCap (large batches) or the
-// batch's big cap, MSD passes beyond.
-#ifndef BMH_DENSE_V2
-#define BMH_DENSE_V2 0
-#endif
-// kWide: the decode-free record layout and k_finish_wide (always with the 9-bit pass; with the
-// 10-bit pass when BMH_DENSE_V2: 4608-rotation buckets, 12-bit digit, 16-bit rests)
-constexpr bool kWide = kG1Bits == 9 || BMH_DENSE_V2;
-#ifndef BMH_WIDE_NT
-#define BMH_WIDE_NT 1024
-#endif
-constexpr uint32_t kDenseNT = kG1Bits == 9 ? BMH_WIDE_NT : 512, kDenseCap = kG1Bits == 9 ? 9216 : 4608,
-                   kDenseDig = kG1Bits == 9 ? 13 : 12;
+// finish workgroup shapes: dense (global-pass buckets of <= kDenseCap rotations, 12-bit digit,
+// R-bit rests), list big (counting-sort finish). List segments over kFinCap take the
+// counting-sort finish up to kSegCap (large batches) or the batch's big cap, MSD passes beyond.
+// (Round 3's 9-bit pass with a wide finish and its persistent LDS-DMA scatter measured slower,
+// DESIGN.md §11; they live in git history, commit dd60b97.)
+constexpr uint32_t kDenseNT = 512, kDenseCap = 4608;
 constexpr uint32_t kSegNT = 512, kSegCap = 4608;
-static_assert(kG1Bits == 9 || kG1Bits == 10, "global-pass digit");
 constexpr uint32_t kFinCap = 4096;  // list segments <= this take the register bitonic sort
 // List segments longer than the batch's big cap take MSD passes (8 bits past their shared prefix
 // per pass); shorter ones over kFinCap a counting-sort finish (12-bit digit + 32-bit ranks).
@@ -347,10 +324,6 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
 // finish resolves rotation bits up to 44; rarer deeper ties go to list passes).
 __device__ __forceinline__ uint32_t rec_pbits(uint32_t n) { return n <= 2 ? 1u : 32u - (uint32_t)__builtin_clz(n - 1); }
 __device__ __forceinline__ uint32_t rec_rbits(uint32_t P) { return min(32u, 44u - P); }
-// The wide finish's record (kG1Bits = 9) needs no decoding: high dword = rotation bits
-// [9, 9 + kRecKeyBits) (its 13-bit digit << 16 | 16-bit rest), low dword = p << 8 | L (blocks
-// of <= 16 MiB) or p (the finish gathers L).
-constexpr uint32_t kRecKeyBits = kDenseDig + 16;
 
 // ------------------------------------------------------------------------- global pass
 // Counting sort of every block by its first kG1Bits rotation bits. Chunks of <= 16 K
@@ -451,16 +424,13 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
         chist[(size_t)blockIdx.x * kG1Bins + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
-// bucket classes in the tagged chunk offsets (bits 30-31)
-constexpr uint32_t kClsSingle = 0u << 30, kClsDense = 1u << 30, kClsList = 2u << 30, kClsBig = 3u << 30;
-constexpr uint32_t kClsMask = 3u << 30;
 // grid = nblocks; one thread per digit: per-chunk write offsets (block-relative, in place),
 // bucket table bk[b][d] = {start, len}; routing of buckets too big for a dense workgroup.
 __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs,
                                                      const uint32_t *__restrict__ bchunks,
                                                      const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
                                                      uint2 *__restrict__ bk, Seg4 *finb, Seg4 *big, Counters *cnt,
-                                                     const uint32_t *__restrict__ loff, uint32_t big_cap, uint32_t tag)
+                                                     const uint32_t *__restrict__ loff, uint32_t big_cap)
 {
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
@@ -478,9 +448,6 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
         for (uint32_t j = 0; j < U; ++j) run += v[j];
     }
     const uint32_t start = block_excl_sum<kG1Bins>(run, s_tmp, nullptr);
-    // tag: each chunk offset also carries the bucket's class in bits 30-31 (blocks < 1 GiB; the
-    // persistent global pass then reads one table per chunk instead of two)
-    const uint32_t cls = !tag ? 0u : run <= 1 ? kClsSingle : run <= kDenseCap ? kClsDense : run > big_cap ? kClsBig : kClsList;
     uint32_t acc = start;
     for (uint32_t k = 0; k < nc; k += U) {
         uint32_t v[U];
@@ -489,7 +456,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j)
             if (k + j < nc) {
-                at(k + j) = acc | cls;
+                at(k + j) = acc;
                 acc += v[j];
             }
     }
@@ -527,7 +494,6 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     const uint8_t *blk = a.data + boff;
     static_assert(kG1Bins <= 1024 && kG1Bits >= 8, "at most one digit per thread");
     const bool tdig = kG1Bins == 1024 || t < kG1Bins;  // this thread owns digit t
-    const bool packL = rec_pbits(n) <= 24;              // (wide records carry the L byte)
     // the chunk's digit offsets and bucket sizes: loads issued together with the text's
     uint32_t cv = 0, bl = 0;
     if (tdig) {
@@ -628,14 +594,9 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint32_t slot = s_off[d] + i;
         const uint32_t blen = s_blen[d];
         if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
-            if constexpr (kWide) {
-                const uint64_t k = (key << (kG1Bits - 8)) >> (64 - kRecKeyBits);
-                rec[boff + slot] = (k << 32) | (packL ? (p << 8) | (uint32_t)(key & 255u) : p);
-            } else {
-                const uint32_t P = rec_pbits(n), R = rec_rbits(P);
-                const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
-                rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
-            }
+            const uint32_t P = rec_pbits(n), R = rec_rbits(P);
+            const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
+            rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
         } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
             // a bucket for the MSD passes: its first pass reads rotation bits [10, 64) from here
@@ -648,283 +609,6 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         }
     }
     GPROF(7);
-}
-
-// ---- persistent global pass with LDS-DMA text staging
-// Workgroup barrier that orders LDS only. An LDS-DMA (global_load_lds) issued before it stays in
-// flight: __syncthreads()' fence would emit vmcnt(0) and drain it (cdna_hip_programming.md
-// "Pipelining across barriers").
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// LDS atomics as inline asm: the compiler waits for every in-flight LDS-DMA (vmcnt(0)) before
-// an LDS atomic it emits itself, which would drain the next chunk's staging.
-typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
-__device__ __forceinline__ void lds_add(uint32_t *p, uint32_t v)
-{
-    asm volatile("ds_add_u32 %0, %1" ::"v"((lds_u32_t *)p), "v"(v) : "memory");
-}
-// eight returning adds of 1, then one wait for all of them
-__device__ __forceinline__ void lds_inc8_rtn(uint32_t *const (&p)[8], uint32_t (&r)[8])
-{
-    asm volatile(
-        "ds_add_rtn_u32 %0, %8, %16\n\tds_add_rtn_u32 %1, %9, %16\n\tds_add_rtn_u32 %2, %10, %16\n\t"
-        "ds_add_rtn_u32 %3, %11, %16\n\tds_add_rtn_u32 %4, %12, %16\n\tds_add_rtn_u32 %5, %13, %16\n\t"
-        "ds_add_rtn_u32 %6, %14, %16\n\tds_add_rtn_u32 %7, %15, %16\n\ts_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
-        : "v"((lds_u32_t *)p[0]), "v"((lds_u32_t *)p[1]), "v"((lds_u32_t *)p[2]), "v"((lds_u32_t *)p[3]),
-          "v"((lds_u32_t *)p[4]), "v"((lds_u32_t *)p[5]), "v"((lds_u32_t *)p[6]), "v"((lds_u32_t *)p[7]), "v"(1u)
-        : "memory");
-}
-
-// block_excl_sum1 with the LDS-only barrier
-template <int NT>
-__device__ __forceinline__ uint32_t block_excl_sum1_lds(uint32_t v, uint32_t *s_tmp)
-{
-    constexpr int NW = NT / 64;
-    check_full_exec();
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t inc = wave_incl_sum_dpp(v);
-    if (lane_id() == 63) s_tmp[w] = inc;
-    lds_barrier();
-    uint32_t pre = 0;
-#pragma unroll
-    for (int j = 0; j < NW; ++j) pre += (uint32_t)j < w ? s_tmp[j] : 0u;
-    return pre + inc - v;
-}
-
-constexpr uint32_t kG1Pieces = (kG1Chunk + 26 + 15) / 16;  // 16-byte text pieces a chunk reads
-
-// The chunk's text piece pc (block bytes start - 16 + 16 pc ..) can be copied as is: inside the
-// block and 16-byte aligned. Otherwise (a block's first / last chunk) it takes the byte path.
-__device__ __forceinline__ bool g1_piece_fast(const uint8_t *blk, const GChunk &ch, uint32_t pc)
-{
-    const int64_t q = (int64_t)ch.start - 16 + 16 * (int64_t)pc;
-    return q >= 0 && q + 16 <= (int64_t)ch.n && (((uintptr_t)(blk + q)) & 15u) == 0;
-}
-// workgroup-uniform: every piece of the chunk is fast
-__device__ __forceinline__ bool g1_chunk_fast(const uint8_t *data, const GChunk &ch)
-{
-    const uint8_t *blk = data + ch.boff;
-    return ch.start >= 16 && (uint64_t)ch.start - 16 + 16ull * ((ch.len + 26 + 15) / 16) <= ch.n &&
-           (((uintptr_t)(blk + ch.start)) & 15u) == 0;
-}
-
-// Loader wave (wave 0 of the workgroup, lane l): LDS-DMA of chunk c's fast text pieces into
-// s_txt and of its tagged offset table (1024 x u32) into s_tbl. Lane-linear destinations.
-__device__ __forceinline__ void g1_load_dma(const uint8_t *data, const GChunk &ch, uint32_t c,
-                                            const uint32_t *__restrict__ chist, uint32_t *s_txt, uint32_t *s_tbl,
-                                            uint32_t l)
-{
-    const uint8_t *blk = data + ch.boff;
-    const uint32_t np = (ch.len + 26 + 15) / 16;
-    for (uint32_t j = 0; 64 * j < np; ++j) {
-        const uint32_t pc = 64 * j + l;
-        if (pc < np && g1_piece_fast(blk, ch, pc))
-            __builtin_amdgcn_global_load_lds(blk + ((int64_t)ch.start - 16 + 16 * (int64_t)pc), s_txt + 4 * 64 * j, 16,
-                                             0, 0);
-    }
-    const uint32_t *row = chist + (size_t)c * kG1Bins;
-#pragma unroll
-    for (uint32_t j = 0; j < kG1Bins / 256; ++j)
-        __builtin_amdgcn_global_load_lds(row + 256 * j + 4 * l, s_tbl + 256 * j, 16, 0, 0);
-}
-
-// The byte path for the pieces the loader skipped (cyclic: wraps around the block).
-__device__ __forceinline__ void g1_stage_fix(const uint8_t *data, const GChunk &ch, uint32_t *s_txt, uint32_t t)
-{
-    const uint8_t *blk = data + ch.boff;
-    const uint32_t np = (ch.len + 26 + 15) / 16;
-    for (uint32_t pc = t; pc < np; pc += 1024) {
-        if (g1_piece_fast(blk, ch, pc)) continue;
-        uint32_t u[4] = {0, 0, 0, 0};
-        const int64_t q = (int64_t)ch.start - 16 + 16 * (int64_t)pc;
-        for (int k = 0; k < 16; ++k) {
-            int64_t r = (q + k) % (int64_t)ch.n;
-            if (r < 0) r += ch.n;
-            u[k >> 2] |= (uint32_t)blk[r] << (8 * (k & 3));
-        }
-        *(uint4 *)&s_txt[4 * pc] = make_uint4(u[0], u[1], u[2], u[3]);
-    }
-}
-
-// One chunk, its text in s_txt and its tagged offsets in s_tbl: the counting sort and record
-// writes of k_g1_scatter, with LDS-only barriers and LDS atomics as inline asm (the loader's
-// DMA of the next chunk stays in flight). The loader wave issues no global stores, so its
-// vmcnt tracks only its DMA; the other waves never wait on vmcnt (their record stores drain
-// in the background). On return s_cnt is zero again.
-__device__ __forceinline__ void g1_chunk(const DataArgs &a, const GChunk &ch, uint32_t t, const uint32_t *s_txt,
-                                         uint32_t *s_tbl, uint16_t *s_ent, uint32_t *s_cnt, uint32_t *s_tmp,
-                                         uint64_t *__restrict__ rec)
-{
-    const uint32_t b = ch.block, boff = ch.boff, n = ch.n;
-    const bool tdig = kG1Bins == 1024 || t < kG1Bins;
-    const bool packL = rec_pbits(n) <= 24;
-    const uint32_t e0 = 16 * t;
-    uint32_t dg[4] = {0, 0, 0, 0}, nx = 0;
-    const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
-    if (nv) {
-        for (int k = 0; k < 4; ++k) dg[k] = s_txt[(e0 >> 2) + 4 + k];
-        if (nv < 16) {
-            const uint32_t j = e0 + 16 + nv;
-            nx = (s_txt[j >> 2] >> (8 * (j & 3u))) & 255u;
-            for (uint32_t k = nv; k < 16; ++k) dg[k >> 2] &= ~(255u << (8 * (k & 3)));
-        } else {
-            nx = s_txt[(e0 >> 2) + 8] & 255u;
-        }
-    }
-    // the 16 digits, two per register (kG1Bins = the sink digit of slots past the chunk)
-    uint32_t dgt2[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 16; k += 2)
-        dgt2[k / 2] = (k < nv ? g1_digit(dg, k, nv, nx) : kG1Bins) | ((k + 1 < nv ? g1_digit(dg, k + 1, nv, nx) : kG1Bins) << 16);
-#pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) lds_add(&s_cnt[(dgt2[k / 2] >> (16 * (k & 1))) & 0xffffu], 1u);
-    lds_barrier();
-    {
-        const uint32_t ex = block_excl_sum1_lds<1024>(tdig ? s_cnt[t] : 0u, s_tmp);
-        if (tdig) {
-            s_tbl[t] -= ex;  // slot of local element i with digit d = offset(d) + i (class bits kept)
-            s_cnt[t] = ex;
-        }
-    }
-    lds_barrier();
-#pragma unroll
-    for (uint32_t h = 0; h < 2; ++h) {  // 8 slot reservations in flight at a time
-        uint32_t *ap[8];
-        uint32_t dst[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) ap[k] = &s_cnt[(dgt2[4 * h + k / 2] >> (16 * (k & 1))) & 0xffffu];
-        lds_inc8_rtn(ap, dst);
-#pragma unroll
-        for (uint32_t k = 0; k < 8; ++k)
-            s_ent[((dgt2[4 * h + k / 2] >> (16 * (k & 1))) & 0xffffu) < kG1Bins ? dst[k] : kG1Chunk] =
-                (uint16_t)(e0 + 8 * h + k);
-    }
-    lds_barrier();
-    if (tdig) s_cnt[t] = 0;  // (not read again this chunk)
-    if (t == 0) s_cnt[kG1Bins] = 0;
-    if (t < 64) return;  // the loader wave issues no global stores
-#pragma unroll 4
-    for (uint32_t i = t - 64; i < ch.len; i += 960) {
-        const uint32_t rel = s_ent[i];
-        const uint32_t p = ch.start + rel;
-        const uint32_t j0 = rel + 15, w0 = j0 >> 2, al = (j0 & 3u) * 8u;
-        const uint32_t d0 = s_txt[w0], d1 = s_txt[w0 + 1], d2 = s_txt[w0 + 2];
-        const uint64_t lo = ((uint64_t)d1 << 32) | d0;
-        const uint64_t v64 = al ? ((lo >> al) | ((uint64_t)d2 << (64 - al))) : lo;
-        const uint64_t b8 = (d2 >> al) & 255u;
-        const uint64_t key = __builtin_bswap64((v64 >> 16) | (b8 << 48)) | (v64 & 255u);
-        const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
-        const uint32_t tv = s_tbl[d], cls = tv & kClsMask;
-        const uint32_t slot = (tv & ~kClsMask) + i;
-        if (cls == kClsDense) {  // the dense finish reads the record, writes SA
-            if constexpr (kWide) {
-                const uint64_t k = (key << (kG1Bits - 8)) >> (64 - kRecKeyBits);
-                rec[boff + slot] = (k << 32) | (packL ? (p << 8) | (uint32_t)(key & 255u) : p);
-            } else {
-                const uint32_t P = rec_pbits(n), R = rec_rbits(P);
-                const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
-                rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
-            }
-        } else if (cls != kClsSingle || a.full_sa) {
-            a.sa[boff + slot] = p;
-            if (cls == kClsBig) rec[boff + slot] = (key << (kG1Bits - 8)) & ~(uint64_t)(kG1Bins - 1);
-        }
-        if (cls == kClsSingle) {
-            a.L[boff + slot] = (uint8_t)key;
-            if (p == 0) a.prim[b] = slot;
-        }
-    }
-}
-
-// Persistent form of k_g1_scatter (blocks < 1 GiB, tagged offsets). Workgroups stay resident and
-// take the chunks of their XCD lane (workgroup i runs on XCD i mod 8) in order from a per-lane
-// counter, so the chunks in flight on an XCD stay consecutive (their per-digit record runs
-// meet in its L2, as with one workgroup per chunk launched in order; a fixed stride per
-// workgroup let them drift apart: 3.3 -> 4.7 ms per GiB). Wave 0 is the loader: it takes part
-// in the LDS phases but issues no global stores; while the other waves write chunk k's records
-// it fetches the next chunk index and descriptor and streams that chunk's text and offset
-// table into the other pair of LDS buffers by LDS-DMA, so the next chunk starts with its data
-// in place (no staging phase). Its vmcnt tracks only its own loads: waiting for the DMA never
-// waits for the record stores.
-struct G1Slot {
-    uint32_t c, block, start, len, boff, n, pad0, pad1;  // c = chunk index (>= nchunks: none left)
-};
-
-// loader wave, lane l: take the lane's next chunk, publish it in `slot`, start its DMA
-__device__ __forceinline__ void g1_fetch(const DataArgs &a, const GChunk *__restrict__ chunks, uint32_t nchunks,
-                                         const uint32_t *__restrict__ chist, uint32_t lane, G1Slot *slot,
-                                         uint32_t *s_txt, uint32_t *s_tbl, uint32_t l)
-{
-    uint32_t k = 0;
-    if (l == 0) k = atomicAdd(&a.cnt->g1next[lane], 1u);
-    const uint32_t c = lane + 8u * (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)k, 0, 64));
-    GChunk g{0, 0, 0, 0, 0, 0, 0, 0};
-    if (c < nchunks) {
-        const GChunk v = chunks[c];
-        g.block = __builtin_amdgcn_readfirstlane(v.block);
-        g.start = __builtin_amdgcn_readfirstlane(v.start);
-        g.len = __builtin_amdgcn_readfirstlane(v.len);
-        g.boff = __builtin_amdgcn_readfirstlane(v.boff);
-        g.n = __builtin_amdgcn_readfirstlane(v.n);
-        if (g.len) g1_load_dma(a.data, g, c, chist, s_txt, s_tbl, l);
-    }
-    if (l == 0) *slot = G1Slot{c, g.block, g.start, g.len, g.boff, g.n, 0, 0};
-}
-
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_g1_scatter_p(
-    DataArgs a, const GChunk *__restrict__ chunks, uint32_t nchunks, const uint32_t *__restrict__ chist,
-    uint64_t *__restrict__ rec)
-{
-    // all LDS in one array (cdna_hip_programming.md: a second __shared__ object can make the
-    // compiler wait for the in-flight LDS-DMA before unrelated LDS accesses)
-    constexpr uint32_t kTxtW = kG1Pieces * 4;  // words per text buffer: byte j <-> block position
-                                               // start - 16 + j (cyclic), 16-byte pieces
-    constexpr uint32_t oA = 0, oB = oA + kTxtW, oTA = oB + kTxtW, oTB = oTA + kG1Bins, oCnt = oTB + kG1Bins,
-                       oSlot = oCnt + kG1Bins + 1, oTmp = oSlot + 16, oEnt = oTmp + 17,
-                       kWords = oEnt + (kG1Chunk + 2) / 2;
-    __shared__ __align__(16) uint32_t s_lds[kWords];
-    static_assert(oTA % 4 == 0 && oTB % 4 == 0, "DMA destinations 16-byte aligned");
-    uint32_t *const s_cnt = s_lds + oCnt, *const s_tmp = s_lds + oTmp;
-    uint16_t *const s_ent = reinterpret_cast<uint16_t *>(s_lds + oEnt);
-    G1Slot *const s_slot = reinterpret_cast<G1Slot *>(s_lds + oSlot);
-    const uint32_t lane = blockIdx.x & 7u;
-    {
-        const uint32_t t = threadIdx.x;
-        if (t < 64) g1_fetch(a, chunks, nchunks, chist, lane, &s_slot[0], s_lds + oA, s_lds + oTA, t);
-        if (kG1Bins == 1024 || t < kG1Bins) s_cnt[t] = 0;
-        if (t == 0) s_cnt[kG1Bins] = 0;
-    }
-    for (uint32_t x = 0;; x ^= 1u) {
-        // the thread index as an opaque value per chunk: per-thread addresses are recomputed in
-        // every step instead of being hoisted out of the loop (they would not fit 64 VGPRs)
-        uint32_t t = threadIdx.x;
-        asm volatile("" : "+v"(t));
-        const bool loader = __builtin_amdgcn_readfirstlane(t >> 6) == 0;
-        uint32_t *const s_txt = s_lds + (x ? oB : oA), *const s_tbl = s_lds + (x ? oTB : oTA);
-        // the chunk of slot x has landed (its DMA was the loader's last VMEM work); every
-        // thread is done with the other buffers
-        if (loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        const G1Slot sl = s_slot[x];
-        GChunk cur;
-        cur.block = __builtin_amdgcn_readfirstlane(sl.block);
-        cur.start = __builtin_amdgcn_readfirstlane(sl.start);
-        cur.len = __builtin_amdgcn_readfirstlane(sl.len);
-        cur.boff = __builtin_amdgcn_readfirstlane(sl.boff);
-        cur.n = __builtin_amdgcn_readfirstlane(sl.n);
-        cur.pad0 = cur.pad1 = cur.pad2 = 0;
-        const uint32_t c = __builtin_amdgcn_readfirstlane(sl.c);
-        if (c >= nchunks) break;  // workgroup-uniform
-        if (cur.len && !g1_chunk_fast(a.data, cur)) {  // a block's first / last chunk: byte path
-            g1_stage_fix(a.data, cur, s_txt, t);
-            lds_barrier();
-        }
-        if (cur.len) g1_chunk(a, cur, t, s_txt, s_tbl, s_ent, s_cnt, s_tmp, rec);
-        // (the other waves are writing chunk c's records now)
-        if (loader) g1_fetch(a, chunks, nchunks, chist, lane, &s_slot[x ^ 1u], s_lds + (x ? oA : oB),
-                             s_lds + (x ? oTA : oTB), t & 63u);
-    }
 }
 
 // ------------------------------------------------------------------------- finish pass
@@ -1539,185 +1223,6 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     __syncthreads();
     DPROF(0);
     finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
-}
-
-// Wide dense finish for kG1Bits = 9 (buckets of ~8192 rotations on random data; the global
-// pass then writes its records in per-digit runs of ~32, half as many cache-line pieces as with
-// 10 bits). 512 threads x IPT elements, kept in two registers each (record = digit << 16 | rest,
-// and p << 8 | L or p: nothing to decode); a DIG-bit LDS counting sort with 16-bit counters, then
-// every element ranks itself inside its sub-bucket by the 16-bit rest (rotation bits up to
-// kG1Bits + DIG + 16). 16-bit rests keep the LDS at < 40 KB: four workgroups per CU. Final slots
-// are parked as L bytes (over the dead counters) and stored in slot order; SA is stored only for
-// the slots a later pass reads (deferred sub-buckets, tie groups) or in full-SA mode.
-template <uint32_t NT, uint32_t CAP, uint32_t DIG>
-__global__ __launch_bounds__(NT) void k_finish_wide(DataArgs a, const uint2 *__restrict__ bk,
-                                                    const uint64_t *__restrict__ rec)
-{
-    constexpr uint32_t IPT = (CAP + NT - 1) / NT;
-    constexpr uint32_t NDIG = 1u << DIG, NW = NDIG / 2, WPT = NW / NT;  // counter words (2 digits each)
-    constexpr uint32_t DMASK = NDIG - 1, KEEP = 1u << 31;
-    static_assert(DIG + 16 == kRecKeyBits && WPT % 4 == 0 && CAP <= 4 * NW && CAP < (1u << (31 - DIG)), "wide shape");
-    __shared__ uint16_t s_rest[CAP + 4];
-    __shared__ __align__(16) uint32_t s_cnt[NW];  // digit counters; then the parked L bytes
-    __shared__ uint32_t s_tmp[NT / 64 + 1];
-    __shared__ DeferQueue<kDeferQ> dq;
-    uint8_t *const s_park = reinterpret_cast<uint8_t *>(s_cnt);
-    const uint32_t x = blockIdx.x & 7u, kb = blockIdx.x >> 3;
-    const uint32_t b = x + 8u * (kb >> kG1Bits);
-    if (b >= a.nb) return;
-    const uint2 e = bk[(size_t)b * kG1Bins + (kb & (kG1Bins - 1))];
-    const uint32_t len = e.y;
-    if (len < 2 || len > CAP) return;
-    const uint32_t t = threadIdx.x;
-    DPROF_START;
-    const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff, gstart = boff + e.x;
-    const bool packL = rec_pbits(n) <= 24;
-    const uint8_t *blk = a.data + boff;
-    // records: every load in flight before the first is used (slots past the bucket read 0)
-    const __amdgpu_buffer_rsrc_t rs = make_rsrc(rec + gstart, len * 8u);
-    uint32_t pl[IPT], dd[IPT];
-#pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        const uint64_t r = buf_load_u64(rs, (t + k * NT) * 8u);
-        dd[k] = (uint32_t)(r >> 32);
-        pl[k] = (uint32_t)r;
-    }
-    for (uint32_t i = t; i < NW; i += NT) s_cnt[i] = 0;
-    if (t == 0) s_tmp[NT / 64] = 0;
-    dq_init(dq);
-    __syncthreads();
-    DPROF(0);
-#pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t d = dd[k] >> 16;
-        if (t + k * NT < len) atomicAdd(&s_cnt[d >> 1], 1u << (16 * (d & 1u)));
-    }
-    __syncthreads();
-    DPROF(1);
-    {
-        // thread t owns counter words WPT*t .. WPT*t + WPT - 1 (read 16 bytes at a time):
-        // counts -> starts
-        uint32_t sum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < WPT; j += 4) {
-            const uint4 w = *reinterpret_cast<const uint4 *>(&s_cnt[WPT * t + j]);
-            sum += (w.x & 0xffffu) + (w.x >> 16) + (w.y & 0xffffu) + (w.y >> 16) + (w.z & 0xffffu) + (w.z >> 16) +
-                   (w.w & 0xffffu) + (w.w >> 16);
-        }
-        uint32_t ex = block_excl_sum1<NT>(sum, s_tmp);
-#pragma unroll
-        for (uint32_t j = 0; j < WPT; j += 4) {
-            uint4 w = *reinterpret_cast<const uint4 *>(&s_cnt[WPT * t + j]);
-            uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t e0 = ex, e1 = ex + (v[q] & 0xffffu);
-                ex = e1 + (v[q] >> 16);
-                v[q] = e0 | (e1 << 16);
-            }
-            *reinterpret_cast<uint4 *>(&s_cnt[WPT * t + j]) = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-    }
-    __syncthreads();
-    DPROF(2);
-#pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        if (t + k * NT < len) {
-            // (an opaque copy: the counting pass's address and shift are recomputed here, not kept
-            // live in registers per element from there)
-            uint32_t h = dd[k];
-            asm volatile("" : "+v"(h));
-            const uint32_t d = h >> 16, sh = 16 * (d & 1u);
-            const uint32_t me = (atomicAdd(&s_cnt[d >> 1], 1u << sh) >> sh) & 0xffffu;
-            s_rest[me] = (uint16_t)h;
-            dd[k] = d | (me << DIG);
-        }
-    }
-    __syncthreads();
-    DPROF(3);
-    // s_cnt now holds every sub-bucket's end; its start is the previous digit's end
-    const uint64_t newbits = (uint64_t)kG1Bits + DIG + 16;
-    const bool final_depth = newbits >= 8ull * n;
-    const bool full_sa = a.full_sa != 0;
-    auto bound_words = [&](uint32_t k, uint32_t &w0, uint32_t &w1) {
-        const uint32_t d = t + k * NT < len ? dd[k] & DMASK : 0u;
-        w1 = s_cnt[d >> 1];
-        w0 = s_cnt[((d - 1) >> 1) & (NW - 1)];
-    };
-    uint32_t nw0, nw1;
-    bound_words(0, nw0, nw1);
-#pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        const uint32_t w0 = nw0, w1 = nw1;
-        if (k + 1 < IPT) bound_words(k + 1, nw0, nw1);
-        if (t + k * NT >= len) continue;
-        const uint32_t d = dd[k] & DMASK, me = dd[k] >> DIG;
-        const uint32_t p = packL ? pl[k] >> 8 : pl[k];
-        const uint32_t s1 = (w1 >> (16 * (d & 1u))) & 0xffffu;
-        const uint32_t s0 = d ? (w0 >> (16 * ((d - 1) & 1u))) & 0xffffu : 0u;
-        const uint32_t m = s1 - s0;
-        if (m > kSmallM) {  // deferred whole, grouped by the digit (its SA is read later)
-            dd[k] = me | KEEP;
-            if (me == s0) dq_push(a, dq, gstart + s0, m, kG1Bits + DIG, b, n);
-            continue;
-        }
-        // rank = #(rest, slot) pairs below this element's; the first four members read together
-        // (m <= 4 for ~99 % of the sub-buckets on random data; this element's own rest is one
-        // of them then), the rest one by one
-        uint32_t c = 0, eqt = 1, r;
-        if (m > 1) {
-            uint32_t rf4[4];
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                rf4[j] = 0;
-                if (j < 2 || s0 + j < s1) rf4[j] = s_rest[s0 + j];
-            }
-            const uint32_t o = me - s0;
-            r = o == 0 ? rf4[0] : o == 1 ? rf4[1] : o == 2 ? rf4[2] : o == 3 ? rf4[3] : (uint32_t)s_rest[me];
-            const uint32_t key = (r << 16) | me;
-            eqt = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const bool in = s0 + j < s1;
-                c += in && ((rf4[j] << 16) | (s0 + j)) < key;
-                eqt += in && rf4[j] == r;
-            }
-#pragma nounroll
-            for (uint32_t f = s0 + 4; f < s1; ++f) {
-                const uint32_t rf = s_rest[f];
-                c += ((rf << 16) | f) < key;
-                eqt += rf == r;
-            }
-        }
-        const uint32_t local = s0 + c;
-        uint32_t gs = local;
-        bool keep = full_sa;
-        if (eqt > 1) {  // tied so far: the group starts after the strictly smaller rests
-            uint32_t lt = 0;
-            for (uint32_t f = s0; f < s1; ++f) lt += s_rest[f] < r;
-            gs = s0 + lt;
-            keep = true;
-            if (c == lt) dq_push(a, dq, gstart + gs, eqt, (uint32_t)newbits, b, n);
-        }
-        dd[k] = local | (keep ? KEEP : 0u);
-        if (p == 0 && (eqt == 1 || final_depth)) a.prim[b] = e.x + gs;
-    }
-    DPROF(4);
-    dq_flush<NT>(a, dq);  // (starts with a barrier: the counters are dead after it)
-    DPROF(5);
-    // slot -> L byte (SA stored here for the slots a later pass reads)
-#pragma unroll
-    for (uint32_t k = 0; k < IPT; ++k) {
-        if (t + k * NT < len) {
-            const uint32_t slot = dd[k] & ~KEEP, p = packL ? pl[k] >> 8 : pl[k];
-            s_park[slot] = packL ? (uint8_t)pl[k] : lastcol_byte(blk, n, p);
-            if (dd[k] & KEEP) a.sa[gstart + slot] = p;
-        }
-    }
-    __syncthreads();
-    DPROF(6);
-    for (uint32_t i = t; i < len; i += NT) a.L[gstart + i] = s_park[i];
-    DPROF(7);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -2773,9 +2278,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     const size_t bcap = ccap[kListBig], dtcap = N / kDTile + bcap + 2;
     static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
     // bitonic list classes merged into two launches per round for latency-bound batches
-    // (BMH_SORT_CLASSES=5 keeps the five shapes: an A/B knob)
-    static const int sort_classes = getenv("BMH_SORT_CLASSES") ? atoi(getenv("BMH_SORT_CLASSES")) : 0;
-    const bool merge_sort_classes = sort_classes == 2 || (sort_classes == 0 && N <= kMergeSortBatch);
+    const bool merge_sort_classes = N <= kMergeSortBatch;
 
     // SA-lite (default): the finish passes store SA only where a later pass reads it. If some
     // block then needs rank doubling (which reads every slot's SA), the data phase is re-run
@@ -2796,24 +2299,13 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
 
         // ---- data phase
         BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
-        // persistent LDS-DMA global pass for blocks < 1 GiB (tagged offsets), else one workgroup per chunk
-        const bool g1p = BMH_SCATTER_P && bt.max_n < (1u << 30);
         BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
-                   d_cnt, d_loff, big_cap, g1p ? 1u : 0u);
+                   d_cnt, d_loff, big_cap);
         set_out(0);
-        if (g1p)
-            BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter_p,
-                       std::min<uint32_t>(nchunks, 8u * cdiv(BMH_G1P_PER_CU * c->cus, 8u)), 1024, 0, da, d_chunks, nchunks,
-                       chist, rec);
-        else
-            BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
+        BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
-        if constexpr (kWide)
-            BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_wide<kDenseNT, kDenseCap, kDenseDig>), 8u * cdiv(nb, 8) * kG1Bins,
-                       kDenseNT, 0, da, bk, rec);
-        else
-            BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<512, 4608>), 8u * cdiv(nb, 8) * kG1Bins, 512, 0, da, bk,
-                       rec);
+        BMH_LAUNCH(c, "bwt_finish_dense", (k_finish_dense<kDenseNT, kDenseCap>), 8u * cdiv(nb, 8) * kG1Bins, kDenseNT, 0,
+                   da, bk, rec);
 #if defined(BMH_PROF_SCATTER) || defined(BMH_PROF_DENSE)
         {
             std::vector<uint32_t> h((1u << 18) * 8);

@@ -139,7 +139,7 @@ def test_run_heavy_blocks_in_four_pipeline_batch(ctx, oracle):
     (Ctx::screen_total), so its run-heavy blocks (1-4 MiB, <= n/4 runs) stay on the rotation sorter
     and never queue behind pipeline 3. Every record equals the same block encoded alone (where the
     screen sends it down the run path), and one block equals the oracle."""
-    sizes = [(4 << 20) - 3 * b * 7919 if b % 3 else (1 << 20) + b * 4099 for b in range(20)]
+    sizes = [(4 << 20) - 3 * b * 7919 if b % 3 else (1 << 20) + b * 4099 for b in range(24)]
     blocks = [_np_runs(100 + b, n, (3, 17, 200)[b % 3], (6.0, 12.0, 40.0)[b % 3]) for b, n in enumerate(sizes)]
     assert sum(sizes) > 64 << 20 and len(blocks) >= 16
     for b in blocks:  # run-heavy by the screen's rule (runs <= n / 4)
