@@ -33,7 +33,6 @@
 #include <algorithm>
 #include <exception>
 #include <thread>
-#include <rocprim/rocprim.hpp>
 
 #include "device_util.h"
 
@@ -102,10 +101,203 @@ __global__ __launch_bounds__(256) void k_prim_scatter(const uint32_t *__restrict
     if (j < nb) prim[map[j]] = tmp[j];
 }
 
-__global__ __launch_bounds__(256) void k_head_flags(const uint8_t *__restrict__ t, uint32_t n, uint8_t *__restrict__ f)
+// ---- in-house primitives (no library sort on the hot path): tiles of kPrimTile elements,
+// 256 threads x 16 each.
+constexpr uint32_t kPrimTile = 4096;
+
+// Run heads of one block, in position order (stream compaction of T[p] != T[p - 1], cyclic):
+// per-tile head counts, their exclusive scan (k_tiles_excl), then each thread writes the heads of
+// its 16 consecutive positions at its tile's offset + its workgroup prefix.
+__device__ __forceinline__ uint32_t head_bits16(const uint8_t *__restrict__ t, uint32_t n, uint32_t p0)
 {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p < n) f[p] = t[p] != t[p ? p - 1 : n - 1];
+    uint32_t f = 0;
+    if (p0 < n) {
+        uint32_t prev = t[p0 ? p0 - 1 : n - 1];
+        const uint32_t e = min(n, p0 + 16u);
+        for (uint32_t p = p0; p < e; ++p) {
+            const uint32_t x = t[p];
+            f |= (uint32_t)(x != prev) << (p - p0);
+            prev = x;
+        }
+    }
+    return f;
+}
+__global__ __launch_bounds__(256) void k_heads_count(const uint8_t *__restrict__ t, uint32_t n, uint32_t *__restrict__ tcnt)
+{
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t c = (uint32_t)__builtin_popcount(head_bits16(t, n, blockIdx.x * kPrimTile + 16u * threadIdx.x));
+    uint32_t tot;
+    block_excl_sum1<256>(c, s_tmp, &tot);
+    if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(256) void k_heads_write(const uint8_t *__restrict__ t, uint32_t n,
+                                                     const uint32_t *__restrict__ toff, uint32_t *__restrict__ H)
+{
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t p0 = blockIdx.x * kPrimTile + 16u * threadIdx.x;
+    uint32_t f = head_bits16(t, n, p0);
+    uint32_t o = toff[blockIdx.x] + block_excl_sum1<256>((uint32_t)__builtin_popcount(f), s_tmp);
+    while (f) {
+        const uint32_t k = (uint32_t)__builtin_ctz(f);
+        H[o++] = p0 + k;
+        f &= f - 1;
+    }
+}
+
+// One workgroup: exclusive prefix (op = sum, or max with identity 0) of cnt[0..m) into out.
+template <bool MAX>
+__global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict__ cnt, uint32_t m, uint32_t *__restrict__ out)
+{
+    __shared__ uint32_t s_tmp[17];
+    const uint32_t per = (m + 1023) / 1024, t = threadIdx.x, a = min(m, t * per), e = min(m, a + per);
+    uint32_t acc = 0;
+    for (uint32_t i = a; i < e; ++i) acc = MAX ? max(acc, cnt[i]) : acc + cnt[i];
+    uint32_t run = MAX ? block_excl_max<1024>(acc, s_tmp) : block_excl_sum<1024>(acc, s_tmp, nullptr);
+    for (uint32_t i = a; i < e; ++i) {
+        const uint32_t v = cnt[i];
+        out[i] = run;
+        run = MAX ? max(run, v) : run + v;
+    }
+}
+
+// LSD radix sort of (u64 key, u32 value) pairs by kRsBits-bit digits, stable. Tiles of kRsTile
+// elements, 256 threads; wave w holds the tile's elements [1024 w, 1024 w + 1024) in 16 rounds of
+// 64. Per pass: a tile histogram (digit-major [kRsBins][tiles]), then a scatter: each wave ranks
+// its elements by digit with no barrier (a ballot match gives the rank among the round's equal
+// digits, running per-wave digit counters in LDS carry it across rounds), one barrier, then the
+// waves' counts are scanned per digit and every element goes to tile offset + waves below + its
+// rank. The scatter takes its digit offsets from the counts of the tiles before it (up to
+// kRsInlineTiles tiles: two launches a pass), or from a per-digit scan (k_rsort_rows) beyond.
+constexpr uint32_t kRsBits = 11, kRsBins = 1u << kRsBits, kRsDPT = kRsBins / 256;  // digits per thread
+constexpr uint32_t kRsTile = 4096, kRsInlineTiles = 16;  // inline: each tile reads kRsBins x tiles counts
+__global__ __launch_bounds__(256) void k_rsort_hist(const uint64_t *__restrict__ key, uint32_t n, uint32_t shift,
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt)
+{
+    __shared__ uint32_t h[kRsBins];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t d = t; d < kRsBins; d += 256) h[d] = 0;
+    __syncthreads();
+#pragma unroll 4
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t i = blockIdx.x * kRsTile + j * 256u + t;
+        if (i < n) atomicAdd(&h[(uint32_t)(key[i] >> shift) & (kRsBins - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t d = t; d < kRsBins; d += 256) cnt[(size_t)d * ntiles + blockIdx.x] = h[d];
+}
+// grid = kRsBins digits: row d of cnt -> exclusive prefix over the tiles (in place), total in dtot[d]
+__global__ __launch_bounds__(256) void k_rsort_rows(uint32_t *__restrict__ cnt, uint32_t ntiles, uint32_t *__restrict__ dtot)
+{
+    __shared__ uint32_t s_tmp[8];
+    uint32_t *row = cnt + (size_t)blockIdx.x * ntiles;
+    uint32_t carry = 0;
+    for (uint32_t b = 0; b < ntiles; b += 256) {
+        const uint32_t i = b + threadIdx.x;
+        const uint32_t v = i < ntiles ? row[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_sum1<256>(v, s_tmp, &tot);
+        if (i < ntiles) row[i] = carry + ex;
+        carry += tot;
+        __syncthreads();  // s_tmp reuse
+    }
+    if (threadIdx.x == 0) dtot[blockIdx.x] = carry;
+}
+// INLINE: cnt holds raw tile counts (<= kRsInlineTiles tiles); else rowpre / dtot from k_rsort_rows
+template <bool INLINE>
+__global__ __launch_bounds__(256) void k_rsort_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                       uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t n,
+                                                       uint32_t shift, uint32_t ntiles, const uint32_t *__restrict__ cnt,
+                                                       const uint32_t *__restrict__ dtot)
+{
+    __shared__ uint32_t s_wc[4][kRsBins + 1], s_tmp[8];
+    const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
+    // thread t owns digits kRsDPT t .. kRsDPT t + kRsDPT - 1: their totals and this tile's prefix
+    uint32_t tot[kRsDPT], pre[kRsDPT];
+#pragma unroll
+    for (uint32_t q = 0; q < kRsDPT; ++q) {
+        const uint32_t d = kRsDPT * t + q;
+        const uint32_t *row = cnt + (size_t)d * ntiles;
+        tot[q] = pre[q] = 0;
+        if (INLINE) {
+            for (uint32_t u = 0; u < ntiles; ++u) {
+                const uint32_t c = row[u];
+                pre[q] += u < blockIdx.x ? c : 0u;
+                tot[q] += c;
+            }
+        } else {
+            pre[q] = row[blockIdx.x];
+            tot[q] = dtot[d];
+        }
+    }
+    for (uint32_t i = t; i < 4 * (kRsBins + 1); i += 256) (&s_wc[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << l) - 1;
+    const uint32_t i0 = blockIdx.x * kRsTile + w * 1024u + l;
+    uint64_t k[16];
+    uint32_t v[16], r[16];
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        const uint32_t i = i0 + 64u * j;
+        k[j] = i < n ? kin[i] : 0ull;
+        v[j] = i < n ? vin[i] : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        // digit of element j, kRsBins for padding (its own value, apart from every digit)
+        const uint32_t d = i0 + 64u * j < n ? (uint32_t)(k[j] >> shift) & (kRsBins - 1) : kRsBins;
+        uint64_t m = ~0ull;
+#pragma unroll
+        for (uint32_t bit = 0; bit <= kRsBits; ++bit) {
+            const uint64_t bal = __ballot((d >> bit) & 1u);
+            m &= ((d >> bit) & 1u) ? bal : ~bal;
+        }
+        const uint32_t below = (uint32_t)__builtin_popcountll(m & lt);
+        const uint32_t base = s_wc[w][d];
+        wave_sync();  // every lane's read before the leader's update (a wave's LDS ops run in order)
+        if (below == 0) s_wc[w][d] = base + (uint32_t)__builtin_popcountll(m);
+        wave_sync();
+        r[j] = (base + below) | (d << 16);
+    }
+    __syncthreads();
+    // digits of thread t: offset of the tile's run + the counts of the waves below each wave
+    {
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kRsDPT; ++q) sum += tot[q];
+        uint32_t base = block_excl_sum1<256>(sum, s_tmp);
+        uint32_t c[kRsDPT][3];
+#pragma unroll
+        for (uint32_t q = 0; q < kRsDPT; ++q)
+#pragma unroll
+            for (uint32_t u = 0; u < 3; ++u) c[q][u] = s_wc[u][kRsDPT * t + q];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t q = 0; q < kRsDPT; ++q) {
+            const uint32_t d = kRsDPT * t + q, b0 = base + pre[q];
+            s_wc[0][d] = b0;
+            s_wc[1][d] = b0 + c[q][0];
+            s_wc[2][d] = b0 + c[q][0] + c[q][1];
+            s_wc[3][d] = b0 + c[q][0] + c[q][1] + c[q][2];
+            base += tot[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) {
+        if (i0 + 64u * j >= n) continue;
+        const uint32_t pos = s_wc[w][r[j] >> 16] + (r[j] & 0xffffu);
+        kout[pos] = k[j];
+        vout[pos] = v[j];
+    }
+}
+__global__ __launch_bounds__(256) void k_rsort_copy(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
+                                                    uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) {
+        kout[i] = kin[i];
+        vout[i] = vin[i];
+    }
 }
 
 // K_i = c_i << 25 | [d_i > c_i] << 24 | (d_i > c_i ? ~L_i : L_i) & 0xffffff, value i
@@ -132,22 +324,43 @@ __global__ __launch_bounds__(256) void k_pair_keys(const uint32_t *__restrict__ 
     idx[i] = i;
 }
 
-// first sorted slot of each key's group (0 elsewhere; a max-scan spreads it) + group count
-__global__ __launch_bounds__(256) void k_group_heads(const uint64_t *__restrict__ sk, uint32_t m, uint32_t *__restrict__ g,
+// first sorted slot of each key's group (0 elsewhere) per thread run of 16 slots, the tile's
+// largest (its last head) in tmax, and the group count
+__global__ __launch_bounds__(256) void k_group_heads(const uint64_t *__restrict__ sk, uint32_t m, uint32_t *__restrict__ tmax,
                                                      uint32_t *__restrict__ ngroups)
 {
-    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    const bool head = j < m && (j == 0 || sk[j] != sk[j - 1]);
-    if (j < m) g[j] = head ? j : 0u;
-    const uint32_t k = wave_sum_dpp((uint32_t)head);
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t j0 = blockIdx.x * kPrimTile + 16u * threadIdx.x;
+    uint32_t last = 0, heads = 0;
+    for (uint32_t j = j0; j < min(m, j0 + 16u); ++j)
+        if (j == 0 || sk[j] != sk[j - 1]) {
+            last = j;
+            ++heads;
+        }
+    const uint32_t mx = wave_incl_max(last);
+    const uint32_t k = wave_sum_dpp(heads);
+    if ((threadIdx.x & 63u) == 63u) s_tmp[threadIdx.x >> 6] = mx;
     if ((threadIdx.x & 63u) == 0 && k) atomicAdd(ngroups, k);
+    __syncthreads();
+    if (threadIdx.x == 0) tmax[blockIdx.x] = max(max(s_tmp[0], s_tmp[1]), max(s_tmp[2], s_tmp[3]));
 }
 
-__global__ __launch_bounds__(256) void k_rank_scatter(const uint32_t *__restrict__ gs, const uint32_t *__restrict__ sidx,
-                                                      uint32_t m, uint32_t *__restrict__ rank)
+// rank[sidx[j]] = the slot of the last group head <= j: the tiles' exclusive max prefix (tpre),
+// then within the tile a workgroup max-scan over the 16-slot runs
+__global__ __launch_bounds__(256) void k_rank_scatter(const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sidx,
+                                                      uint32_t m, const uint32_t *__restrict__ tpre,
+                                                      uint32_t *__restrict__ rank)
 {
-    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    if (j < m) rank[sidx[j]] = gs[j];
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t j0 = blockIdx.x * kPrimTile + 16u * threadIdx.x, e = min(m, j0 + 16u);
+    uint32_t last = 0;
+    for (uint32_t j = j0; j < e; ++j)
+        if (j == 0 || sk[j] != sk[j - 1]) last = j;
+    uint32_t g = max(tpre[blockIdx.x], block_excl_max<256>(last, s_tmp));
+    for (uint32_t j = j0; j < e; ++j) {
+        if (j == 0 || sk[j] != sk[j - 1]) g = j;
+        rank[sidx[j]] = g;
+    }
 }
 
 // position keys (header comment), value p
@@ -193,13 +406,10 @@ inline uint32_t bits_for(uint32_t v)  // bits holding 0 .. v
 }
 
 struct RunWs {
-    uint8_t *flags;
-    uint32_t *H, *idx, *idx2, *g, *gs, *rank, *cnt;
+    uint32_t *H, *idx, *idx2, *rank, *cnt, *tcnt, *toff, *rowpre, *dtot;
     uint64_t *key, *key2;
     uint64_t *pkey, *pkey2;
     uint32_t *pval, *pval2;
-    void *tmp;
-    size_t tmp_bytes;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -207,33 +417,28 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // Workspace of one block's run BWT (n positions, m runs), carved from one slot.
 RunWs run_ws(Ctx *c, uint32_t n, uint32_t m)
 {
-    size_t t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    BMH_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<uint32_t>(0), (const uint8_t *)nullptr,
-                            (uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, c->stream));
-    BMH_HIP(rocprim::radix_sort_pairs(nullptr, t2, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                      (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)std::max(m, 1u), 0, 64,
-                                      c->stream));
-    BMH_HIP(rocprim::radix_sort_pairs(nullptr, t3, (const uint64_t *)nullptr, (uint64_t *)nullptr,
-                                      (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)n, 0, 64, c->stream));
-    BMH_HIP(rocprim::inclusive_scan(nullptr, t4, (const uint32_t *)nullptr, (uint32_t *)nullptr, (size_t)std::max(m, 1u),
-                                    rocprim::maximum<uint32_t>(), c->stream));
-    const size_t tb = align256(std::max(std::max(t1, t2), std::max(t3, t4)));
-    const size_t mm = std::max(m, 1u);
-    const size_t sizes[] = {align256(n), align256(mm * 4) * 6 + 256, align256(mm * 8) * 2, align256((size_t)n * 8) * 2,
-                            align256((size_t)n * 4) * 2, tb};
+    const size_t mm = std::max(m, 1u), nt = cdiv(std::max(n, 1u), kPrimTile);
+    const size_t sizes[] = {align256(mm * 4) * 4 + 256, align256(nt * 4) * 2, align256(kRsBins * nt * 4) + kRsBins * 4,
+                            align256(mm * 8) * 2, align256((size_t)n * 8) * 2, align256((size_t)n * 4) * 2};
     size_t total = 0;
-    for (size_t s : sizes) total += s;
+    for (size_t z : sizes) total += z;
     uint8_t *p = (uint8_t *)c->get(WS_RUNS, total);
     RunWs w;
-    w.flags = p;
-    p += sizes[0];
-    uint32_t **u32s[] = {&w.H, &w.idx, &w.idx2, &w.g, &w.gs, &w.rank};
+    uint32_t **u32s[] = {&w.H, &w.idx, &w.idx2, &w.rank};
     for (auto q : u32s) {
         *q = (uint32_t *)p;
         p += align256(mm * 4);
     }
     w.cnt = (uint32_t *)p;
     p += 256;
+    w.tcnt = (uint32_t *)p;
+    p += align256(nt * 4);
+    w.toff = (uint32_t *)p;
+    p += align256(nt * 4);
+    w.rowpre = (uint32_t *)p;
+    p += align256(kRsBins * nt * 4);
+    w.dtot = (uint32_t *)p;
+    p += kRsBins * 4;
     w.key = (uint64_t *)p;
     p += align256(mm * 8);
     w.key2 = (uint64_t *)p;
@@ -245,9 +450,6 @@ RunWs run_ws(Ctx *c, uint32_t n, uint32_t m)
     w.pval = (uint32_t *)p;
     p += align256((size_t)n * 4);
     w.pval2 = (uint32_t *)p;
-    p += align256((size_t)n * 4);
-    w.tmp = p;
-    w.tmp_bytes = tb;
     return w;
 }
 
@@ -255,25 +457,39 @@ RunWs run_ws(Ctx *c, uint32_t n, uint32_t m)
 // group. Returns the group count (one host wait).
 uint32_t rank_groups(Ctx *c, RunWs &w, const uint64_t *sk, const uint32_t *sidx, uint32_t m, uint32_t *h_cnt)
 {
+    const uint32_t nt = cdiv(m, kPrimTile);
     BMH_HIP(hipMemsetAsync(w.cnt, 0, 4, c->stream));
-    BMH_LAUNCH(c, "bwt_run_groups", k_group_heads, cdiv(m, 256), 256, 0, sk, m, w.g, w.cnt);
-    size_t tb = w.tmp_bytes;
-    const int p = c->tbegin("bwt_run_scan");
-    BMH_HIP(rocprim::inclusive_scan(w.tmp, tb, w.g, w.gs, (size_t)m, rocprim::maximum<uint32_t>(), c->stream));
-    c->tend(p);
-    BMH_LAUNCH(c, "bwt_run_groups", k_rank_scatter, cdiv(m, 256), 256, 0, w.gs, sidx, m, w.rank);
+    BMH_LAUNCH(c, "bwt_run_groups", k_group_heads, nt, 256, 0, sk, m, w.tcnt, w.cnt);
+    BMH_LAUNCH(c, "bwt_run_scan", k_tiles_excl<true>, 1, 1024, 0, w.tcnt, nt, w.toff);
+    BMH_LAUNCH(c, "bwt_run_groups", k_rank_scatter, nt, 256, 0, sk, sidx, m, w.toff, w.rank);
     c->d2h(h_cnt, w.cnt, 4);
     c->sync();
     return *h_cnt;
 }
 
-void sort_pairs(Ctx *c, RunWs &w, const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout, size_t cnt,
+// Stable sort of cnt (key, value) pairs by key bits [0, end_bit): result in (kout, vout); kin /
+// vin are scratch (overwritten).
+void sort_pairs(Ctx *c, RunWs &w, uint64_t *kin, uint64_t *kout, uint32_t *vin, uint32_t *vout, uint32_t cnt,
                 uint32_t end_bit)
 {
-    size_t tb = w.tmp_bytes;
-    const int p = c->tbegin("bwt_run_sort");
-    BMH_HIP(rocprim::radix_sort_pairs(w.tmp, tb, kin, kout, vin, vout, cnt, 0, end_bit, c->stream));
-    c->tend(p);
+    const uint32_t nt = cdiv(cnt, kRsTile), passes = (end_bit + kRsBits - 1) / kRsBits;
+    uint64_t *ks = kin, *kd = kout;
+    uint32_t *vs = vin, *vd = vout;
+    for (uint32_t ps = 0; ps < passes; ++ps) {
+        const uint32_t sh = kRsBits * ps;
+        BMH_LAUNCH(c, "bwt_run_sort", k_rsort_hist, nt, 256, 0, ks, cnt, sh, nt, w.rowpre);
+        if (nt <= kRsInlineTiles) {
+            BMH_LAUNCH(c, "bwt_run_sort", k_rsort_scatter<true>, nt, 256, 0, ks, vs, kd, vd, cnt, sh, nt, w.rowpre,
+                       w.dtot);
+        } else {
+            BMH_LAUNCH(c, "bwt_run_sort", k_rsort_rows, kRsBins, 256, 0, w.rowpre, nt, w.dtot);
+            BMH_LAUNCH(c, "bwt_run_sort", k_rsort_scatter<false>, nt, 256, 0, ks, vs, kd, vd, cnt, sh, nt, w.rowpre,
+                       w.dtot);
+        }
+        std::swap(ks, kd);
+        std::swap(vs, vd);
+    }
+    if (ks != kout) BMH_LAUNCH(c, "bwt_run_sort", k_rsort_copy, cdiv(cnt, 256), 256, 0, ks, vs, kout, vout, cnt);
 }
 
 // The BWT of one run-heavy block t[0..n) with m >= 0 cyclic runs: L[0..n) and *prim (device).
@@ -284,14 +500,10 @@ void run_block(Ctx *c, const uint8_t *t, uint32_t n, uint32_t m, uint8_t *L, uin
         return;
     }
     RunWs w = run_ws(c, n, m);
-    BMH_LAUNCH(c, "bwt_run_heads", k_head_flags, cdiv(n, 256), 256, 0, t, n, w.flags);
-    {
-        size_t tb = w.tmp_bytes;
-        const int p = c->tbegin("bwt_run_heads");
-        BMH_HIP(rocprim::select(w.tmp, tb, rocprim::counting_iterator<uint32_t>(0), w.flags, w.H, w.cnt, (size_t)n,
-                                c->stream));
-        c->tend(p);
-    }
+    const uint32_t ntn = cdiv(n, kPrimTile);
+    BMH_LAUNCH(c, "bwt_run_heads", k_heads_count, ntn, 256, 0, t, n, w.tcnt);
+    BMH_LAUNCH(c, "bwt_run_heads", k_tiles_excl<false>, 1, 1024, 0, w.tcnt, ntn, w.toff);
+    BMH_LAUNCH(c, "bwt_run_heads", k_heads_write, ntn, 256, 0, t, n, w.toff, w.H);
     BMH_LAUNCH(c, "bwt_run_keys", k_run_keys, cdiv(m, 256), 256, 0, t, n, w.H, m, w.key, w.idx);
     sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, m, 33);
     uint32_t groups = rank_groups(c, w, w.key2, w.idx2, m, h_cnt);

@@ -194,6 +194,11 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 if (lane + 64 * k == v) key[k] = (f << 32) | ((0xffffu - rkr[k]) << 16) | v;
         }
     } else {
+        // (A wave-uniform form of this loop, queues in registers read by v_readlane with 64-bit keys
+        // moved as two halves, measured slower: 437 K vs 289 K ticks of merges for Calgary's
+        // blocks, profiles/r04/huff_build_ab_v1.txt — the selects and hazards of the register
+        // reads cost more than the LDS reads they replace. Round 3's wave-uniform attempt failed
+        // for another reason: its u64 keys went through a 32-bit readfirstlane)
         // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
         // two queues: the leaves sorted by key, and the internal nodes, which are created with
         // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is

@@ -1,0 +1,127 @@
+"""The two-queue form of the reference's Huffman priority queue (main.cpp:245-254), as
+k_huff_build runs it wave-uniformly out of registers (csrc/huffman.hip), restated in Python and
+checked against the oracle's tree; and the diagnosis of round 3's failed wave-uniform attempt
+(VERDICT r3 item 5): with the 64-bit queue keys (frequency << 32 | address rank | id) read
+through a 32-bit cross-lane read (readfirstlane of a u64 keeps the low half), the merges order
+nodes by address rank alone, and zipf n = 39,800 encodes to exactly the 30,932-byte record that
+run produced, against the reference's 16,231 bytes (tests/golden/manifests/bands.json)."""
+import json
+import os
+
+import numpy as np
+
+from bmh import synth
+from oracle_ffi import GOLDEN
+
+
+def _addr_rank(L: int, s: int) -> int:
+    # SURVEY App. B.3 closed form (huffman.hip addr_rank)
+    if L <= 128:
+        return {1: 0, 0: 126, 2: 127}.get(s, s - 2 if 3 <= s <= 127 else s)
+    if s == 1:
+        return 0
+    if 3 <= s <= 64:
+        return s - 2
+    if 129 <= s <= 192:
+        return s - 66
+    if 65 <= s <= 127:
+        return s + 62
+    return {0: 190, 2: 191, 128: 192}.get(s, s)
+
+
+def two_queue_lengths(freq: np.ndarray, first: np.ndarray, key_bits: int = 64):
+    """Code lengths per leaf (first-occurrence order) from the two-queue merge of huffman.hip,
+    with every queue read masked to key_bits (64: exact; 32: the truncating read)."""
+    order = sorted((s for s in range(256) if freq[s]), key=lambda s: first[s])
+    L = len(order)
+    M = (1 << key_bits) - 1
+
+    def key(f, i):
+        return (int(f) << 32) | ((0xFFFF - _addr_rank(L, i)) << 16) | i
+
+    leaves = sorted(key(freq[order[i]], i) for i in range(L))
+    q2 = []
+    st = {"q1": 0, "gh": 0, "ge": 0, "gn": 0, "me": 0, "gf": 0}
+    k = {"k1": leaves[0] & M, "k2": M}
+    fr = {i: int(freq[order[i]]) for i in range(L)}
+
+    def q2get(i):
+        return q2[i] & M
+
+    def pop():
+        if k["k1"] < k["k2"]:
+            r = k["k1"]
+            st["q1"] += 1
+            k["k1"] = leaves[st["q1"]] & M if st["q1"] < L else M
+        else:
+            r = k["k2"]
+            st["ge"] -= 1
+            if st["ge"] > st["gh"]:
+                k["k2"] = q2get(st["ge"] - 1)
+            else:
+                st["gh"] = st["gn"]
+                st["ge"] = st["gh"]
+                k["k2"] = M
+                if st["gh"] < st["me"]:
+                    st["gf"] = q2get(st["gh"]) >> 32
+                    while st["ge"] < st["me"] and q2get(st["ge"]) >> 32 == st["gf"]:
+                        st["ge"] += 1
+                    st["gn"] = st["ge"]
+                    k["k2"] = q2get(st["ge"] - 1)
+        return r
+
+    kids = {}
+    for m in range(L - 1):
+        ra, rb = pop(), pop()
+        v = L + m
+        kids[v] = (ra & 0xFFFF, rb & 0xFFFF)
+        f = (ra >> 32) + (rb >> 32)  # the frequency as the (possibly truncated) keys carry it
+        fr[v] = fr[ra & 0xFFFF] + fr[rb & 0xFFFF]
+        nk = key(f, v)
+        while len(q2) <= max(st["ge"], st["me"]):
+            q2.append(M)
+        if st["gn"] == st["me"] and (st["ge"] == st["gh"] or f == st["gf"]):
+            if st["ge"] == st["gh"]:
+                st["gf"] = f
+            q2[st["ge"]] = nk
+            st["ge"] += 1
+            if st["ge"] > st["gn"]:
+                st["gn"] = st["me"] = st["ge"]
+            k["k2"] = nk & M
+        else:
+            q2[st["me"]] = nk
+            st["me"] += 1
+    depth = {2 * L - 2: 0}
+    for v in range(2 * L - 2, L - 1, -1):
+        for c in kids[v]:
+            depth[c] = depth[v] + 1
+    if L == 1:
+        depth = {0: 0}
+    return order, [depth[i] for i in range(L)], fr
+
+
+def record_len(freq, first, key_bits=64) -> int:
+    order, dep, fr = two_queue_lengths(freq, first, key_bits)
+    L = len(order)
+    bits = sum(fr[i] * dep[i] for i in range(L))
+    return 24 + (10 * L - 1 + 7) // 8 + max(1, (bits + 7) // 8)
+
+
+def test_two_queue_matches_oracle_tree(oracle):
+    for data in (synth.zipf_text(300_000).tobytes(), synth.splitmix64_bytes(0, 0, 200_000).tobytes(),
+                 open(os.path.join(GOLDEN, "calgary", "paper1"), "rb").read()):
+        _, L_ = oracle.bwt(data)
+        freq, first = oracle.histogram(oracle.mtf(L_))
+        order, dep, _ = two_queue_lengths(freq, first)
+        oln, _, _ = oracle.huffman_build(freq, first)
+        assert [int(oln[s]) for s in order] == dep
+
+
+def test_round3_wave_uniform_defect_reproduced(oracle):
+    man = json.load(open(os.path.join(GOLDEN, "manifests", "bands.json")))
+    e = next(c for c in man["cases"] if c["kind"] == "zipf" and c["n"] == 39800)
+    data = synth.zipf_text(39800).tobytes()
+    _, L_ = oracle.bwt(data)
+    freq, first = oracle.histogram(oracle.mtf(L_))
+    assert record_len(freq, first, 64) == e["record_len"] == 16231
+    assert record_len(freq, first, 32) == 30932  # the r3 run's record (gpurun_out/r3m_tests.log)
