@@ -53,7 +53,7 @@ enum Slot : int {
     WS_CHIST, WS_BSTART, WS_COUNTERS, WS_LTILES, WS_LTHIST, WS_LSEGS, WS_SEGOR, WS_COOP, WS_LISTS, WS_L, WS_MTF,
     WS_MTF_R, WS_MTF_S, WS_MTF_SUPER, WS_MTF_CHUNKS, WS_FREQ, WS_FIRST, WS_PRIMARY, WS_PACK_BITS,
     WS_PACK_CHUNKS, WS_TABLES, WS_HDR, WS_HDR_OFFS, WS_IN, WS_OUT, WS_IN2, WS_OUT2, WS_IN3, WS_OUT3, WS_RESOLVED, WS_FIN_CUR, WS_FIN_NXT,
-    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_BAND, WS_SYNTH, WS_COUNT_
+    WS_DSEG_CUR, WS_DSEG_NXT, WS_DLARGE, WS_DLARGE2, WS_DGROUPS, WS_KEY8, WS_ROFFS, WS_STATUS, WS_PACK_HIST, WS_FINT_CUR, WS_FINT_NXT, WS_FINB_CUR, WS_FINB_NXT, WS_KEY8B, WS_RUN_MISC, WS_RUN_MOVE, WS_RUN_IN, WS_RUN_L, WS_RUNS, WS_RUN_PRIM, WS_BAND, WS_SYNTH, WS_ALPHA, WS_COUNT_
 };
 
 struct Ctx {

@@ -97,7 +97,7 @@ constexpr uint32_t kRunMode = 1u << 30;
 #endif
 constexpr uint32_t kMsdBits = BMH_MSD_BITS, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
 static_assert(kMsdBins >= 65 && kMsdBins <= 1024, "MSD digit (run-mode digits 0..64)");
-constexpr uint32_t kWinShift = 16, kG1WinBits = 64 - kG1Bits;
+constexpr uint32_t kWinShift = 16;
 __device__ __forceinline__ uint32_t seg_known(uint32_t w) { return (w >> kWinShift) & 127u; }
 
 struct Counters {
@@ -158,6 +158,8 @@ struct DataArgs {
     uint32_t *lcnt;      // their counters (cnt->lc[parity], [class][lane]; groups: cnt->lgroups)
     const uint32_t *loff;  // [class][lane] first entry of each lane's sub-list (9 per class)
     Counters *cnt;
+    const uint32_t *ainfo;  // per block: 0 = raw 10-bit global digit, else s | k << 8 (g1_alpha)
+    const uint8_t *arank;   // per block: 256-entry byte -> rank map of a compacted alphabet
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
     uint32_t big_cap;  // list segments longer than this take MSD passes (kBigCapLarge / kBigCapSmall)
 };
@@ -323,7 +325,25 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
 // largest position and R = min(32, 44 - P) (4 MiB blocks: P = 22, R = 22, so one dense
 // finish resolves rotation bits up to 44; rarer deeper ties go to list passes).
 __device__ __forceinline__ uint32_t rec_pbits(uint32_t n) { return n <= 2 ? 1u : 32u - (uint32_t)__builtin_clz(n - 1); }
-__device__ __forceinline__ uint32_t rec_rbits(uint32_t P) { return min(32u, 44u - P); }
+// R also keeps db + 12 + R within the 64 rotation bits the global pass reads (db <= 24)
+__device__ __forceinline__ uint32_t rec_rbits(uint32_t P, uint32_t db) { return min(min(32u, 44u - P), 52u - db); }
+
+// Per-block global-pass alphabet: a block of k <= 32 distinct bytes keys its
+// global pass on s = 2 (k <= 32) or 3 (k <= 10) whole symbols, each replaced by its rank among the
+// block's distinct bytes (order-preserving), mixed radix k: digit = ((r0 k + r1) k + r2) < k^s <=
+// 1024. Every rotation of a bucket then shares its first s bytes, i.e. db = 8 s raw rotation bits
+// (text: 2 characters, against 1 character + 2 bits of the raw 10-bit digit, where every
+// lowercase letter has the same top bits); later passes stay in raw bits. info = s | k << 8,
+// 0 for the raw digit (db = kG1Bits).
+__device__ __forceinline__ uint32_t g1_db(uint32_t info) { return info ? 8u * (info & 255u) : kG1Bits; }
+__device__ __forceinline__ uint32_t g1_digit3(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t info, const uint8_t *rk)
+{
+    if (!info) return (b0 << (kG1Bits - 8)) | (b1 >> (16 - kG1Bits));
+    const uint32_t k = info >> 8;
+    uint32_t d = rk[b0] * k + rk[b1];
+    if ((info & 255u) == 3) d = d * k + rk[b2];
+    return d;
+}
 
 // ------------------------------------------------------------------------- global pass
 // Counting sort of every block by its first kG1Bits rotation bits. Chunks of <= 16 K
@@ -351,11 +371,55 @@ __device__ __forceinline__ uint32_t byte_of(const uint32_t (&dg)[4], uint32_t k)
     return (dg[k >> 2] >> (8 * (k & 3))) & 255u;
 }
 
-// digit of chunk element k (< nv) from its byte and the next one (nx = the byte after the run)
-__device__ __forceinline__ uint32_t g1_digit(const uint32_t (&dg)[4], uint32_t k, uint32_t nv, uint32_t nx)
+// digit of chunk element k (< nv) from its byte and the next two (nx, nx2 = the bytes after the run)
+__device__ __forceinline__ uint32_t g1_digit(const uint32_t (&dg)[4], uint32_t k, uint32_t nv, uint32_t nx, uint32_t nx2,
+                                             uint32_t info, const uint8_t *rk)
 {
     const uint32_t b1 = k + 1 < nv ? byte_of(dg, k + 1) : nx;
-    return (byte_of(dg, k) << (kG1Bits - 8)) | (b1 >> (16 - kG1Bits));
+    const uint32_t b2 = k + 2 < nv ? byte_of(dg, k + 2) : k + 2 == nv ? nx : nx2;
+    return g1_digit3(byte_of(dg, k), b1, b2, info, rk);
+}
+
+// Census of each block's distinct bytes, from the global pass's raw histograms (every position's
+// byte is the first byte of its rotation's digit): k_g1_hist stores each chunk's 256-bit set
+// (plain stores, 8 words a chunk: no atomics on a block's few words from its hundreds of
+// chunks), k_g1_census_fin ORs a block's chunk sets and decides its alphabet, and a second
+// k_g1_hist launch recounts the chunks of the blocks that take compacted digits (the others'
+// workgroups exit at once).
+constexpr uint32_t kAlphaMax = 32;
+// grid = nblocks: the block's alphabet info and rank map from its chunks' sets (list indices
+// c0 + 8k); a compacted block appends its chunks to the recount list
+__global__ __launch_bounds__(256) void k_g1_census_fin(const uint32_t *__restrict__ cbits,
+                                                       const uint32_t *__restrict__ bchunks,
+                                                       const uint32_t *__restrict__ bchunk0,
+                                                       uint32_t *__restrict__ ainfo, uint8_t *__restrict__ arank,
+                                                       uint32_t *__restrict__ rlist)
+{
+    __shared__ uint32_t s_w[8];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint32_t c0 = bchunk0[b], nc = bchunks[b];
+    if (t < 8) s_w[t] = 0;
+    __syncthreads();
+    uint32_t acc = 0;
+    for (uint32_t k = t >> 3; k < nc; k += 32) acc |= cbits[(size_t)(c0 + 8 * k) * 8 + (t & 7u)];
+    if (acc) atomicOr(&s_w[t & 7u], acc);
+    __syncthreads();
+    uint32_t k = 0, below = 0;
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t c = __builtin_popcount(s_w[j]);
+        k += c;
+        if (j < (t >> 5)) below += c;
+    }
+    below += __builtin_popcount(s_w[t >> 5] & ((1u << (t & 31u)) - 1u));
+    const bool compact = k <= kAlphaMax && k >= 1;
+    arank[(size_t)b * 256 + t] = (uint8_t)below;
+    if (t == 0) ainfo[b] = compact ? ((k <= 10 ? 3u : 2u) | (k << 8)) : 0u;
+    if (compact) {  // the block's chunks go on the recount list (rlist[-1] = its length)
+        __shared__ uint32_t s_base;
+        if (t == 0) s_base = atomicAdd(rlist - 1, nc);
+        __syncthreads();
+        for (uint32_t j = t; j < nc; j += 256) rlist[s_base + j] = c0 + 8 * j;
+    }
 }
 
 // Phase timing (experiment builds only): -DBMH_PROF_SCATTER times k_g1_scatter's phases,
@@ -392,36 +456,69 @@ __device__ uint32_t g_dprof[(1u << 18) * 8];
 #define DPROF_START
 #endif
 
-// grid = chunk list; 1024 threads x 16 positions.
+// 1024 threads x 16 positions a chunk. recount = 0 (grid = the chunk list): raw 10-bit digits
+// for every block, plus the census (bits); recount = 1 (a grid of <= 2048 striding over rlist,
+// the chunks of compacted blocks k_g1_census_fin listed): those chunks' digits by the block's
+// alphabet (ainfo / arank) — on a batch with none, a few thousand workgroups read a zero count.
 __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
-                                                  const GChunk *__restrict__ chunks, uint32_t *__restrict__ chist)
+                                                  const GChunk *__restrict__ chunks, uint32_t *__restrict__ rlist,
+                                                  uint32_t *__restrict__ chist, const uint32_t *__restrict__ ainfo,
+                                                  const uint8_t *__restrict__ arank, uint32_t *__restrict__ bits,
+                                                  uint32_t recount)  // bits: 8 words a chunk
 {
     __shared__ uint32_t h[4][kG1Bins];
-    const GChunk ch = chunks[blockIdx.x];
-    if (ch.len == 0) return;
+    __shared__ uint8_t s_rk[256];
     const uint32_t t = threadIdx.x, w = (t >> 6) & 3u;
-    for (uint32_t i = t; i < 4 * kG1Bins; i += 1024) (&h[0][0])[i] = 0;
-    __syncthreads();
-    const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
-    const uint8_t *blk = data + boff;
-    const uint32_t e = 16 * t;
-    if (e < ch.len) {
-        uint32_t dg[4];
-        g1_load16(blk, ch.start, ch.len, e, dg);
-        const uint32_t nv = min(16u, ch.len - e);
-        // the byte after the run: at most one past the block's end (cyclic), no division
-        const uint32_t ni = ch.start + e + nv;
-        const uint32_t nx = blk[ni >= n ? ni - n : ni];
-        if (nv == 16) {
+    uint32_t *const rcount = rlist - 1;  // rlist[-1] = its length, zeroed by the raw pass
+    if (!recount && blockIdx.x == 0 && t == 0) *rcount = 0;
+    const uint32_t nsel = recount ? *rcount : 1u;
+    for (uint32_t q = recount ? blockIdx.x : 0u; q < nsel; q += recount ? gridDim.x : 1u) {
+        const uint32_t ci = recount ? rlist[q] : blockIdx.x;
+        const GChunk ch = chunks[ci];
+        if (ch.len == 0) {
+            if (t < 8) bits[(size_t)ci * 8 + t] = 0;  // an empty chunk's set (never listed)
+            continue;
+        }
+        const uint32_t info = recount ? ainfo[ch.block] : 0u;
+        __syncthreads();                 // the previous chunk's reads of h / s_rk
+        for (uint32_t i = t; i < 4 * kG1Bins; i += 1024) (&h[0][0])[i] = 0;
+        if (info && t < 256) s_rk[t] = arank[(size_t)ch.block * 256 + t];
+        __syncthreads();
+        const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
+        const uint8_t *blk = data + boff;
+        const uint32_t e = 16 * t;
+        if (e < ch.len) {
+            uint32_t dg[4];
+            g1_load16(blk, ch.start, ch.len, e, dg);
+            const uint32_t nv = min(16u, ch.len - e);
+            // the two bytes after the run (cyclic; n may be 1 or 2)
+            const uint32_t ni = (ch.start + e + nv) % n, ni2 = (ni + 1) % n;
+            const uint32_t nx = blk[ni], nx2 = blk[ni2];
+            if (nv == 16) {
 #pragma unroll
-            for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dg, k, 16, nx)], 1u);
-        } else {
-            for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx)], 1u);
+                for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dg, k, 16, nx, nx2, info, s_rk)], 1u);
+            } else {
+                for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx, nx2, info, s_rk)], 1u);
+            }
+        }
+        __syncthreads();
+        static_assert(kG1Bins == 1024, "one digit a thread");
+        const uint32_t sum = h[0][t] + h[1][t] + h[2][t] + h[3][t];
+        chist[(size_t)ci * kG1Bins + t] = sum;
+        if (!recount) {
+            // the chunk's bytes: byte v is present iff one of the digits 4v .. 4v + 3 is counted
+            static_assert(kG1Bits == 10, "census: 4 raw digits per first byte");
+            __syncthreads();
+            h[0][t] = sum;
+            __syncthreads();
+            if (t < 256) {
+                const bool present = (h[0][4 * t] | h[0][4 * t + 1] | h[0][4 * t + 2] | h[0][4 * t + 3]) != 0;
+                const uint64_t bal = __ballot(present);
+                const uint32_t l = t & 63u;
+                if (l < 2) bits[(size_t)ci * 8 + 2 * (t >> 6) + l] = (uint32_t)(bal >> (32 * l));
+            }
         }
     }
-    __syncthreads();
-    for (uint32_t d = t; d < kG1Bins; d += 1024)
-        chist[(size_t)blockIdx.x * kG1Bins + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
 }
 
 // grid = nblocks; one thread per digit: per-chunk write offsets (block-relative, in place),
@@ -430,7 +527,8 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
                                                      const uint32_t *__restrict__ bchunks,
                                                      const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
                                                      uint2 *__restrict__ bk, Seg4 *finb, Seg4 *big, Counters *cnt,
-                                                     const uint32_t *__restrict__ loff, uint32_t big_cap)
+                                                     const uint32_t *__restrict__ loff, uint32_t big_cap,
+                                                     const uint32_t *__restrict__ ainfo)
 {
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
@@ -464,12 +562,13 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     const uint32_t x = b & 7u;  // the block's XCD lane sub-lists (parity 0)
     // buckets <= kDenseCap are the dense finish's; longer ones take MSD passes, or the
     // counting-sort list finish up to big_cap
+    const uint32_t db = g1_db(ainfo[b]);  // the bucket's shared prefix (raw bits), 64 - db window bits known
     if (run > kDenseCap && run > big_cap)
         big[loff[kListBig * 9 + x] + wave_append(&cnt->lc[0][kListBig][x])] =
-            make_uint4(boffs[b] + start, run, kG1Bits, b | (kG1WinBits << kWinShift));
+            make_uint4(boffs[b] + start, run, db, b | ((64u - db) << kWinShift));
     else if (run > kDenseCap)
         finb[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
-            make_uint4(boffs[b] + start, run, kG1Bits, b);
+            make_uint4(boffs[b] + start, run, db, b);
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -486,11 +585,14 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     __shared__ uint32_t s_cnt[kG1Bins + 1], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
     // (s_cnt[kG1Bins]: sink digit of the slots past the chunk, so the LDS phases run unbranched)
     __shared__ uint32_t s_tmp[17];
+    __shared__ uint8_t s_rk[256];
     const GChunk ch = chunks[blockIdx.x];
     if (ch.len == 0) return;
     GPROF_START;
     const uint32_t t = threadIdx.x;
     const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t info = a.ainfo[b], db = g1_db(info);
+    if (info && t < 256) s_rk[t] = a.arank[(size_t)b * 256 + t];
     const uint8_t *blk = a.data + boff;
     static_assert(kG1Bins <= 1024 && kG1Bits >= 8, "at most one digit per thread");
     const bool tdig = kG1Bins == 1024 || t < kG1Bins;  // this thread owns digit t
@@ -541,22 +643,19 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     __syncthreads();
     GPROF(0);
     const uint32_t e0 = 16 * t;
-    uint32_t dg[4] = {0, 0, 0, 0}, nx = 0;
+    uint32_t dg[4] = {0, 0, 0, 0}, nx = 0, nx2 = 0;
     const uint32_t nv = e0 < ch.len ? min(16u, ch.len - e0) : 0u;
     if (nv) {
         // bytes e0 .. e0 + 16 of the chunk = s_txt bytes e0 + 16 .. e0 + 32 (dword aligned)
         for (int k = 0; k < 4; ++k) dg[k] = s_txt[(e0 >> 2) + 4 + k];
-        if (nv < 16) {
-            const uint32_t j = e0 + 16 + nv;
-            nx = (s_txt[j >> 2] >> (8 * (j & 3u))) & 255u;
-            for (uint32_t k = nv; k < 16; ++k) dg[k >> 2] &= ~(255u << (8 * (k & 3)));
-        } else {
-            nx = s_txt[(e0 >> 2) + 8] & 255u;
-        }
+        const uint32_t j = e0 + 16 + nv;
+        nx = (s_txt[j >> 2] >> (8 * (j & 3u))) & 255u;
+        nx2 = (s_txt[(j + 1) >> 2] >> (8 * ((j + 1) & 3u))) & 255u;
+        for (uint32_t k = nv; k < 16; ++k) dg[k >> 2] &= ~(255u << (8 * (k & 3)));
     }
     uint32_t dgt[16];
 #pragma unroll
-    for (uint32_t k = 0; k < 16; ++k) dgt[k] = k < nv ? g1_digit(dg, k, nv, nx) : kG1Bins;
+    for (uint32_t k = 0; k < 16; ++k) dgt[k] = k < nv ? g1_digit(dg, k, nv, nx, nx2, info, s_rk) : kG1Bins;
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) atomicAdd(&s_cnt[dgt[k]], 1u);
     __syncthreads();
@@ -590,18 +689,20 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint64_t v64 = al ? ((lo >> al) | ((uint64_t)d2 << (64 - al))) : lo;  // bytes j0 .. j0 + 7
         const uint64_t b8 = (d2 >> al) & 255u;                                       // byte j0 + 8
         const uint64_t key = __builtin_bswap64((v64 >> 16) | (b8 << 48)) | (v64 & 255u);
-        const uint32_t d = (((uint32_t)(v64 >> 8) & 255u) << (kG1Bits - 8)) | (((uint32_t)(v64 >> 16) & 255u) >> (16 - kG1Bits));
+        const uint32_t d = g1_digit3((uint32_t)(v64 >> 8) & 255u, (uint32_t)(v64 >> 16) & 255u,
+                                     (uint32_t)(v64 >> 24) & 255u, info, s_rk);
         const uint32_t slot = s_off[d] + i;
         const uint32_t blen = s_blen[d];
         if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
-            const uint32_t P = rec_pbits(n), R = rec_rbits(P);
-            const uint64_t sub = ((key >> 8) >> (42 - R)) & ((1ull << (12 + R)) - 1);
+            // rotation bits [db, db + 12 + R) (key >> 8 holds bits [8, 64))
+            const uint32_t P = rec_pbits(n), R = rec_rbits(P, db);
+            const uint64_t sub = ((key >> 8) >> (52 - db - R)) & ((1ull << (12 + R)) - 1);
             rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
         } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
             // a bucket for the MSD passes: its first pass reads rotation bits [10, 64) from here
             // (MSB-aligned, low kG1Bits bits zero) instead of gathering them (kG1WinBits known)
-            if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << (kG1Bits - 8)) & ~(uint64_t)(kG1Bins - 1);
+            if (blen > kDenseCap && blen > a.big_cap) rec[boff + slot] = (key << (db - 8)) & ~((1ull << db) - 1);
         }
         if (blen == 1) {
             a.L[boff + slot] = (uint8_t)key;
@@ -1197,7 +1298,8 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     const uint32_t t = threadIdx.x;
     DPROF_START;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-    const uint32_t P = rec_pbits(n), R = rec_rbits(P);
+    const uint32_t db = __builtin_amdgcn_readfirstlane(g1_db(a.ainfo[b]));  // uniform (keeps it out of VGPRs)
+    const uint32_t P = rec_pbits(n), R = __builtin_amdgcn_readfirstlane(rec_rbits(P, db));
     const bool packL = P <= 24;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     if (t == 0) s_tmp[NT / 64 + 1] = 0;
@@ -1222,7 +1324,7 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     }
     __syncthreads();
     DPROF(0);
-    finish_core<NT, CAP>(a, boff + e.x, e.y, kG1Bits, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+    finish_core<NT, CAP>(a, boff + e.x, e.y, db, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
@@ -2229,6 +2331,12 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
     uint64_t *rec = (uint64_t *)c->get(WS_KEY8, N * 8);
     uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
+    // per-chunk byte sets (8 words a chunk) | per-block alphabet info | rank maps
+    // | recount list length + chunk list
+    uint8_t *d_alpha = (uint8_t *)c->get(WS_ALPHA, (size_t)nchunks * 36 + (size_t)nb * (4 + 256) + 64);
+    uint32_t *abits = (uint32_t *)d_alpha, *ainfo = abits + 8 * (size_t)nchunks;
+    uint8_t *arank = (uint8_t *)(ainfo + nb);
+    uint32_t *rlist = (uint32_t *)(arank + (size_t)nb * 256) + 1;
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list; the finish
@@ -2260,6 +2368,8 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     da.prim = d_prim;
     da.bflag = bflag;
     da.cnt = d_cnt;
+    da.ainfo = ainfo;
+    da.arank = arank;
     // list buffers of the two parities: parity 0 holds what the global pass and the dense finish
     // defer (round 1's input); round r reads parity (r - 1) & 1 and appends to parity r & 1
     Seg4 *const lt[2] = {fint_a, fint_b}, *const lf[2] = {fin_a, fin_b}, *const lb[2] = {finb_a, finb_b};
@@ -2298,9 +2408,15 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                    (uint32_t *)d_cnt, kCntWords);
 
         // ---- data phase
-        BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, chist);
+        // raw digits + each block's byte census, the blocks' alphabets, then the chunks of compacted
+        // blocks recounted
+        BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo, arank,
+                   abits, 0u);
+        BMH_LAUNCH(c, "bwt_g1_census", k_g1_census_fin, nb, 256, 0, abits, d_bchunks, d_bchunk0, ainfo, arank, rlist);
+        BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), 1024, 0, d_in, d_boffs, d_chunks,
+                   rlist, chist, ainfo, arank, abits, 1u);
         BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
-                   d_cnt, d_loff, big_cap);
+                   d_cnt, d_loff, big_cap, ainfo);
         set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries

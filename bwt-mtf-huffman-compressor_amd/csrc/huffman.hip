@@ -73,6 +73,15 @@ __device__ __forceinline__ uint64_t heap_key(uint64_t freq, uint32_t L, uint32_t
 {
     return (freq << 32) | ((0xffffu - addr_rank(L, id)) << 16) | id;
 }
+// The same for an internal node v >= L, branch-free (addr_rank's chain of cases compiles to a
+// run of scalar branches inside the sequential merge loop): L <= 128: [.., 3..127 -> v - 2, 128..
+// -> v] (v = 2 only for L = 2: rank 127); L > 128: [129..192 -> v - 66, 193.. -> v].
+__device__ __forceinline__ uint64_t heap_key_internal(uint64_t freq, uint32_t L, uint32_t v)
+{
+    const uint32_t small = L <= 128u;
+    const uint32_t r = small ? (v == 2u ? 127u : v - 2u * (uint32_t)(v <= 127u)) : v - 66u * (uint32_t)(v <= 192u);
+    return (freq << 32) | ((0xffffu - r) << 16) | v;
+}
 
 // Rank of each of this lane's keys (slots lane + 64k) among the 256 keys of s_keys (padding
 // entries ~0): the number of smaller keys. Keys are read two at a time, 8 loads in flight.
@@ -258,7 +267,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 const uint64_t f = (ra >> 32) + (rb >> 32);
                 s_left[v] = (int16_t)(ra & 0xffffu);
                 s_right[v] = (int16_t)(rb & 0xffffu);
-                const uint64_t nk = heap_key(f, L, v);
+                const uint64_t nk = heap_key_internal(f, L, v);
                 if (gn == me && (ge == gh || (uint32_t)f == gf)) {
                     // the queue is empty, or the node joins the last (= first) group: it pops first
                     if (ge == gh) gf = (uint32_t)f;

@@ -818,3 +818,54 @@ def test_checked_build_full_exec():
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res == {"mismatches": 0, "exec_violations": 0}, res
+
+
+def _alpha_block(rng, n, k, kind):
+    """n bytes over k distinct values (spread over 0..255), as random draws or runs of words."""
+    vals = np.sort(rng.choice(256, k, replace=False)).astype(np.uint8)
+    if kind == "uniform":
+        idx = rng.integers(0, k, n)
+    else:  # Zipf-like words: repeated short patterns
+        words = [rng.integers(0, k, int(rng.integers(2, 9))) for _ in range(50)]
+        seq, tot = [], 0
+        while tot < n:
+            w = words[min(int(rng.zipf(1.3)) - 1, 49)]
+            seq.append(w)
+            tot += w.size
+        idx = np.concatenate(seq)[:n]
+    return vals[idx].tobytes()
+
+
+def test_compacted_alphabet_global_pass(ctx, oracle):
+    """blocks of k <= 32 distinct bytes key the global pass on s whole symbols
+    (s = 3 for k <= 10, 2 for k <= 32; ranks among the block's bytes, db = 8 s) instead of 10 raw
+    bits. Boundary alphabets (1, 2, 10, 11, 32, 33 distinct bytes), tiny blocks, uniform and
+    word-like text, values spread over the byte range, all in one batch past the run screen's
+    batch size (so no block takes the run path): BWT and records equal the oracle's."""
+    rng = np.random.default_rng(2024)
+    blocks, rec_check = [], []
+    for k in (1, 2, 3, 4, 10, 11, 26, 27, 32, 33):
+        for n in (1, 2, 3, 17, 5000, 300_001):
+            blocks.append(_alpha_block(rng, n, k, "uniform" if n % 2 else "words"))
+        rec_check.append(len(blocks) - 1)
+        if k >= 3:
+            blocks.append(_alpha_block(rng, 1 << 20, k, "words"))
+            rec_check.append(len(blocks) - 1)
+    blocks.append(synth.zipf_text(3 << 20).tobytes())
+    rec_check.append(len(blocks) - 1)
+    pad = synth.splitmix64_bytes(0, 0, 70 << 20).tobytes()  # a random block: the batch is past the run screen
+    allb = blocks + [pad]
+    offs = np.zeros(len(allb) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(b) for b in allb])
+    d_in, d_L = ctx.alloc(int(offs[-1])), ctx.alloc(int(offs[-1]))
+    d_in.upload(np.frombuffer(b"".join(allb), np.uint8))
+    prim = ctx.bwt_dev(d_in, offs, d_L)
+    L = d_L.download()
+    d_in.free()
+    d_L.free()
+    for i, b in enumerate(blocks):
+        op, oL = oracle.bwt(b)
+        assert int(prim[i]) == op and L[int(offs[i]):int(offs[i + 1])].tobytes() == oL, (i, len(b), len(set(b)))
+    recs = ctx.encode_blocks(allb)
+    for i in rec_check:
+        assert recs[i] == oracle.encode(blocks[i]), (i, len(blocks[i]))
