@@ -122,6 +122,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ uint64_t s_pcode[512];                  // path bits to the jump target (left 0, right 1)
     __shared__ uint64_t s_lkey[256];                   // leaf keys, then left-aligned leaf codes
     __shared__ uint64_t s_k1[256], s_q2[256];          // leaves in pop order; internal-node queue
+    __shared__ uint16_t s_gs[256];                     // internal-node queue: group start slots
     __shared__ uint32_t s_err;
     uint8_t *s_tree = (uint8_t *)s_tree32;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -163,44 +164,49 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     if (ro != kModelOrder) {
         // the internal nodes' ranks need not ascend, so the queue is simulated as it is: every
         // live node's key in a register slot (node v: lane v & 63, slot v >> 6), each pop a
-        // wave-wide minimum (smallest frequency, then the larger address rank)
+        // wave-wide minimum (smallest frequency, then the larger address rank). The blocks here
+        // are below kBandCeil = 2^17 bytes, so a key fits 32 bits: frequency (< 2^17) << 9 |
+        // 511 - rank (ranks < 2L - 1 <= 511 are distinct, so keys are too, and the popped node is
+        // the one lane slot holding the minimum)
+        static_assert(kBandCeil <= (1u << 17), "32-bit heap-history keys");
         const uint16_t *rk = rrank + ro;
-        uint64_t key[8];
+        uint32_t key[8];
         uint32_t rkr[8];  // the ranks of this lane's nodes (id = lane + 64 k), all loads at once
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) rkr[k] = lane + 64 * k < 2 * L - 1 ? rk[lane + 64 * k] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {
             const uint32_t id = lane + 64 * k;
-            key[k] = id < L ? ((uint64_t)s_freq[s_order[id]] << 32) | ((0xffffu - rkr[k]) << 16) | id : ~0ull;
+            key[k] = id < L ? (s_freq[s_order[id]] << 9) | (511u - rkr[k]) : ~0u;
         }
         for (uint32_t m = 0; m + 1 < L; ++m) {
-            uint64_t r[2];
+            uint32_t r[2], f = 0;
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                uint64_t mn = key[0];
+                uint32_t mn = key[0];
 #pragma unroll
-                for (int k = 1; k < 8; ++k) mn = key[k] < mn ? key[k] : mn;
+                for (int k = 1; k < 8; ++k) mn = min(mn, key[k]);
 #pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const uint64_t o = __shfl_xor(mn, off, 64);
-                    mn = o < mn ? o : mn;
-                }
-                r[t] = mn;
-                const uint32_t id = (uint32_t)(mn & 0xffffu);
+                for (int off = 32; off >= 1; off >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+                uint32_t mine = ~0u;
 #pragma unroll
                 for (uint32_t k = 0; k < 8; ++k)
-                    if (lane + 64 * k == id) key[k] = ~0ull;
+                    if (key[k] == mn) {
+                        key[k] = ~0u;
+                        mine = lane + 64 * k;
+                    }
+                const uint64_t bal = __ballot(mine != ~0u);
+                r[t] = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)__builtin_ctzll(bal));
+                f += mn >> 9;
             }
             const uint32_t v = L + m;
-            const uint64_t f = (r[0] >> 32) + (r[1] >> 32);
             if (lane == 0) {
-                s_left[v] = (int16_t)(r[0] & 0xffffu);
-                s_right[v] = (int16_t)(r[1] & 0xffffu);
+                s_left[v] = (int16_t)r[0];
+                s_right[v] = (int16_t)r[1];
             }
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k)  // the owning lane builds the new node's key
-                if (lane + 64 * k == v) key[k] = (f << 32) | ((0xffffu - rkr[k]) << 16) | v;
+                if (lane + 64 * k == v) key[k] = (f << 9) | (511u - rkr[k]);
         }
     } else {
         // (A wave-uniform form of this loop, queues in registers read by v_readlane with 64-bit keys
@@ -225,20 +231,25 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         __syncthreads();
         HPROF(5);  // (model path) leaf keys ranked
         if (lane == 0) {
-            uint32_t q1 = 0;                      // next leaf
+            uint32_t q1 = 0;                          // next leaf
             uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
-            // queue heads kept in registers with the entry behind each (its LDS read is issued a pop
-            // ahead of its use): k1 = s_k1[q1], k1n = s_k1[q1 + 1]; k2 = s_q2[ge - 1], k2b =
-            // s_q2[ge - 2] while that is still in the first group (else ~0)
-            uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k2 = ~0ull, k2b = ~0ull;
-            uint32_t gf = 0;                      // first group's frequency
+            // queue heads kept in registers with the entries behind them, their LDS reads issued
+            // two pops ahead of use: k1 = s_k1[q1], k1n = s_k1[q1 + 1], k1m = s_k1[q1 + 2]; k2 =
+            // s_q2[ge - 1], k2b = s_q2[ge - 2] while that is still in the first group (else ~0)
+            uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k1m = L > 2 ? s_k1[2] : ~0ull;
+            uint64_t k2 = ~0ull, k2b = ~0ull;
+            uint32_t gf = 0, lf = 0;  // first group's frequency; the last slot's
+            // start slots of the groups after the first, in order (gq = the next one's entry): a
+            // group's end is the next start, no scan over its slots
+            uint32_t gq = 0, ngs = 0;
             auto pop = [&]() -> uint64_t {
                 uint64_t r;
                 if (k1 < k2) {
                     r = k1;
                     ++q1;
                     k1 = k1n;
-                    k1n = q1 + 1 < L ? s_k1[q1 + 1] : ~0ull;
+                    k1n = k1m;
+                    k1m = q1 + 2 < L ? s_k1[q1 + 2] : ~0ull;
                 } else {
                     r = k2;
                     --ge;
@@ -251,11 +262,12 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                         k2 = ~0ull;
                         k2b = ~0ull;
                         if (gh < me) {
-                            gf = (uint32_t)(s_q2[gh] >> 32);
-                            while (ge < me && (uint32_t)(s_q2[ge] >> 32) == gf) ++ge;
+                            ++gq;  // s_gs[gq - 1] == gh
+                            ge = gq < ngs ? (uint32_t)s_gs[gq] : me;
                             gn = ge;
                             k2 = s_q2[ge - 1];
                             k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
+                            gf = (uint32_t)(k2 >> 32);
                         }
                     }
                 }
@@ -276,8 +288,11 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                     if (ge > gn) gn = me = ge;
                     k2 = nk;
                 } else {
-                    s_q2[me++] = nk;  // a later group
+                    // a later group: a new one unless it has the last slot's frequency
+                    if (gn == me || (uint32_t)f != lf) s_gs[ngs++] = (uint16_t)me;
+                    s_q2[me++] = nk;
                 }
+                lf = (uint32_t)f;
             }
         }
     }

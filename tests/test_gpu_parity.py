@@ -825,6 +825,14 @@ def _alpha_block(rng, n, k, kind):
     vals = np.sort(rng.choice(256, k, replace=False)).astype(np.uint8)
     if kind == "uniform":
         idx = rng.integers(0, k, n)
+    elif kind == "repeats":  # slices of one base text: ties tens to hundreds of symbols deep
+        base = rng.integers(0, k, 6000)
+        parts, tot = [], 0
+        while tot < n:
+            a = int(rng.integers(0, 5600))
+            parts.append(base[a:a + int(rng.integers(40, 400))])
+            tot += parts[-1].size
+        idx = np.concatenate(parts)[:n]
     else:  # Zipf-like words: repeated short patterns
         words = [rng.integers(0, k, int(rng.integers(2, 9))) for _ in range(50)]
         seq, tot = [], 0
@@ -839,8 +847,9 @@ def _alpha_block(rng, n, k, kind):
 def test_compacted_alphabet_global_pass(ctx, oracle):
     """blocks of k <= 32 distinct bytes key the global pass on s whole symbols
     (s = 3 for k <= 10, 2 for k <= 32; ranks among the block's bytes, db = 8 s) instead of 10 raw
-    bits. Boundary alphabets (1, 2, 10, 11, 32, 33 distinct bytes), tiny blocks, uniform and
-    word-like text, values spread over the byte range, all in one batch past the run screen's
+    bits; their list rounds compare windows of w-bit symbol ranks (12 .. 16 symbols). Boundary
+    alphabets (1, 2, 10, 11, 32, 33 distinct bytes), tiny blocks, uniform, word-like and
+    deep-repeat text, values spread over the byte range, all in one batch past the run screen's
     batch size (so no block takes the run path): BWT and records equal the oracle's."""
     rng = np.random.default_rng(2024)
     blocks, rec_check = [], []
@@ -851,6 +860,10 @@ def test_compacted_alphabet_global_pass(ctx, oracle):
         if k >= 3:
             blocks.append(_alpha_block(rng, 1 << 20, k, "words"))
             rec_check.append(len(blocks) - 1)
+        # deep ties: the list rounds' compacted windows (w = 1 .. 5 bits a symbol, 12 .. 16
+        # symbols a window, partial-byte starts from the dense finish's deferrals)
+        blocks.append(_alpha_block(rng, 200_003, k, "repeats"))
+        rec_check.append(len(blocks) - 1)
     blocks.append(synth.zipf_text(3 << 20).tobytes())
     rec_check.append(len(blocks) - 1)
     pad = synth.splitmix64_bytes(0, 0, 70 << 20).tobytes()  # a random block: the batch is past the run screen

@@ -1,6 +1,8 @@
 """The two-queue form of the reference's Huffman priority queue (main.cpp:245-254), as
-k_huff_build runs it wave-uniformly out of registers (csrc/huffman.hip), restated in Python and
-checked against the oracle's tree; and the diagnosis of round 3's failed wave-uniform attempt
+k_huff_build's lane-0 loop runs it (csrc/huffman.hip: sorted leaves; internal nodes in frequency
+groups popped newest first, the group starts kept in a FIFO), restated in Python and checked
+against the oracle's tree, on real blocks and on random frequency vectors full of ties; and the
+diagnosis of round 3's failed wave-uniform attempt
 (VERDICT r3 item 5): with the 64-bit queue keys (frequency << 32 | address rank | id) read
 through a 32-bit cross-lane read (readfirstlane of a u64 keeps the low half), the merges order
 nodes by address rank alone, and zipf n = 39,800 encodes to exactly the 30,932-byte record that
@@ -39,35 +41,32 @@ def two_queue_lengths(freq: np.ndarray, first: np.ndarray, key_bits: int = 64):
     def key(f, i):
         return (int(f) << 32) | ((0xFFFF - _addr_rank(L, i)) << 16) | i
 
-    leaves = sorted(key(freq[order[i]], i) for i in range(L))
-    q2 = []
-    st = {"q1": 0, "gh": 0, "ge": 0, "gn": 0, "me": 0, "gf": 0}
+    leaves = sorted(key(freq[order[i]], i) for i in range(L)) + [M, M, M]
+    q2 = [M] * 256
+    gs = []  # start slots of the groups after the first (huffman.hip s_gs), gq = next entry
+    st = {"q1": 0, "gh": 0, "ge": 0, "gn": 0, "me": 0, "gf": 0, "lf": 0, "gq": 0}
     k = {"k1": leaves[0] & M, "k2": M}
     fr = {i: int(freq[order[i]]) for i in range(L)}
-
-    def q2get(i):
-        return q2[i] & M
 
     def pop():
         if k["k1"] < k["k2"]:
             r = k["k1"]
             st["q1"] += 1
-            k["k1"] = leaves[st["q1"]] & M if st["q1"] < L else M
+            k["k1"] = leaves[st["q1"]] & M
         else:
             r = k["k2"]
             st["ge"] -= 1
             if st["ge"] > st["gh"]:
-                k["k2"] = q2get(st["ge"] - 1)
-            else:
-                st["gh"] = st["gn"]
-                st["ge"] = st["gh"]
+                k["k2"] = q2[st["ge"] - 1] & M
+            else:  # the first group is used up: the next starts at gn, ends at the next start
+                st["gh"] = st["ge"] = st["gn"]
                 k["k2"] = M
                 if st["gh"] < st["me"]:
-                    st["gf"] = q2get(st["gh"]) >> 32
-                    while st["ge"] < st["me"] and q2get(st["ge"]) >> 32 == st["gf"]:
-                        st["ge"] += 1
-                    st["gn"] = st["ge"]
-                    k["k2"] = q2get(st["ge"] - 1)
+                    assert gs[st["gq"]] == st["gh"]
+                    st["gq"] += 1
+                    st["ge"] = st["gn"] = gs[st["gq"]] if st["gq"] < len(gs) else st["me"]
+                    k["k2"] = q2[st["ge"] - 1] & M
+                    st["gf"] = k["k2"] >> 32
         return r
 
     kids = {}
@@ -78,8 +77,6 @@ def two_queue_lengths(freq: np.ndarray, first: np.ndarray, key_bits: int = 64):
         f = (ra >> 32) + (rb >> 32)  # the frequency as the (possibly truncated) keys carry it
         fr[v] = fr[ra & 0xFFFF] + fr[rb & 0xFFFF]
         nk = key(f, v)
-        while len(q2) <= max(st["ge"], st["me"]):
-            q2.append(M)
         if st["gn"] == st["me"] and (st["ge"] == st["gh"] or f == st["gf"]):
             if st["ge"] == st["gh"]:
                 st["gf"] = f
@@ -89,8 +86,11 @@ def two_queue_lengths(freq: np.ndarray, first: np.ndarray, key_bits: int = 64):
                 st["gn"] = st["me"] = st["ge"]
             k["k2"] = nk & M
         else:
+            if st["gn"] == st["me"] or f != st["lf"]:
+                gs.append(st["me"])
             q2[st["me"]] = nk
             st["me"] += 1
+        st["lf"] = f
     depth = {2 * L - 2: 0}
     for v in range(2 * L - 2, L - 1, -1):
         for c in kids[v]:
@@ -115,6 +115,24 @@ def test_two_queue_matches_oracle_tree(oracle):
         order, dep, _ = two_queue_lengths(freq, first)
         oln, _, _ = oracle.huffman_build(freq, first)
         assert [int(oln[s]) for s in order] == dep
+
+
+def test_two_queue_matches_oracle_on_tied_frequencies(oracle):
+    """Random frequency vectors drawn from small ranges (long runs of equal frequencies, so many
+    internal-node groups of several members) and every alphabet size class of the address-rank
+    model (L <= 128, > 128, 1, 2, 256)."""
+    rng = np.random.default_rng(7)
+    for trial in range(300):
+        L = int(rng.choice([1, 2, 3, 5, 17, 64, 127, 128, 129, 130, 200, 255, 256]))
+        hi = int(rng.choice([1, 2, 3, 5, 40, 1000]))
+        freq = np.zeros(256, np.uint32)
+        syms = rng.choice(256, L, replace=False)
+        freq[syms] = rng.integers(1, hi + 1, L)
+        first = np.full(256, 0xFFFFFFFF, np.uint32)
+        first[syms] = rng.permutation(L * 7)[:L]
+        order, dep, _ = two_queue_lengths(freq, first)
+        oln, _, _ = oracle.huffman_build(freq, first)
+        assert [int(oln[s]) for s in order] == dep, (trial, L, hi)
 
 
 def test_round3_wave_uniform_defect_reproduced(oracle):
