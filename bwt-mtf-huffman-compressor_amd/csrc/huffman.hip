@@ -316,9 +316,12 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         s_pcode[c] = 1;
     }
     __syncthreads();
-    for (uint32_t round = 0; round < 9; ++round) {  // depth <= 255 < 2^9
+    // depth <= 255 < 2^9: at most 9 rounds; done as soon as every target is the root (a code
+    // tree of depth D takes ceil(log2 D) rounds: ~5 for a 256-leaf tree)
+    for (uint32_t round = 0; round < 9; ++round) {
         uint32_t na[8], nd[8];
         uint64_t nc[8];
+        bool more = false;
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k) {  // all reads of the round before any write
             const uint32_t v = lane + 64 * k;
@@ -333,6 +336,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 na[k] = a2;
                 nd[k] = d + d2;
                 nc[k] = d >= 64 ? c : (c2 << d) | c;  // (longer paths are flagged below)
+                more |= a2 != nn - 1;
             }
         }
         __syncthreads();
@@ -346,6 +350,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
             }
         }
         __syncthreads();
+        if (!__any(more)) break;  // one wave: the exit is uniform
     }
     HPROF(2);  // pointer jumping
     // leaves: code book, and the left-aligned codes, whose order is the preorder of the leaves
