@@ -205,46 +205,6 @@ __device__ __forceinline__ uint64_t rot_window(const uint8_t *__restrict__ blk, 
     return w;
 }
 
-// List windows of a block with a compacted alphabet (ainfo k >= 2, round 4): the rest of the
-// current byte as raw bits, then c whole symbols as their w-bit ranks among the block's k bytes
-// (w = bits of k - 1, c = min(16, (64 - psh) / w): 12 symbols of a 27-letter text where raw
-// windows hold 8). The rank map is monotone, so the window orders and ties exactly as the raw
-// bytes it covers; a tie run goes on adv = psh + 8c raw bits deeper (symbol-aligned from then).
-struct CWin {
-    uint32_t w, c, psh;  // w = 0: raw 64-bit windows
-};
-__device__ __forceinline__ CWin cwin_shape(const DataArgs &a, uint32_t b, uint32_t db)
-{
-    const uint32_t k = a.ainfo[b] >> 8;
-    if (k < 2) return CWin{0u, 0u, 0u};
-    const uint32_t w = 32u - (uint32_t)__builtin_clz(k - 1), psh = (8u - (db & 7u)) & 7u;
-    return CWin{w, min(16u, (64u - psh) / w), psh};
-}
-__device__ __forceinline__ uint32_t cwin_adv(const CWin &s) { return s.w ? s.psh + 8u * s.c : 64u; }
-__device__ __forceinline__ uint64_t list_window(const DataArgs &a, const uint8_t *__restrict__ blk, uint32_t n,
-                                                uint32_t b, uint32_t p, uint32_t db, const CWin &s)
-{
-    if (!s.w) return rot_window(blk, n, p, db);
-    const uint8_t *__restrict__ rk = a.arank + (size_t)b * 256;
-    uint32_t q = (uint32_t)(((uint64_t)p + (db >> 3)) % n);
-    uint64_t key = 0;
-    if (s.psh) {
-        key = blk[q] & ((1u << s.psh) - 1u);
-        if (++q == n) q = 0;
-    }
-    if (q + s.c <= n) {
-#pragma unroll
-        for (uint32_t i = 0; i < 16; ++i)
-            if (i < s.c) key = (key << s.w) | rk[blk[q + i]];
-    } else {
-        for (uint32_t i = 0; i < s.c; ++i) {
-            key = (key << s.w) | rk[blk[q]];
-            if (++q == n) q = 0;
-        }
-    }
-    return key << (64u - s.psh - s.c * s.w);
-}
-
 // The lists a deferred segment can go to.
 // The first four are refilled every round; the groups list grows over the whole data phase.
 enum : uint32_t { kListTiny = 0, kListFin = 1, kListFinb = 2, kListBig = 3, kListGroups = 4, kNumLists = 5 };
@@ -971,7 +931,7 @@ __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__r
                 const uint32_t db = __shfl((int)sgl.z, (int)sl, 64), b = __shfl((int)sgl.w, (int)sl, 64);
                 const uint32_t len = slen * (uint32_t)live;
                 const uint32_t idx = l - pos;
-                uint32_t p = 0, boff = 0, n = 1, adv = 64;
+                uint32_t p = 0, boff = 0, n = 1;
                 uint64_t key = ~0ull;
                 const uint8_t *blk = a.data;
                 if (live) {
@@ -979,9 +939,7 @@ __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__r
                     n = a.boffs[b + 1] - boff;
                     blk = a.data + boff;
                     p = a.sa[gstart + idx];
-                    const CWin cw = cwin_shape(a, b, db);
-                    adv = cwin_adv(cw);
-                    key = list_window(a, blk, n, b, p, db, cw);
+                    key = rot_window(blk, n, p, db);
                 }
                 uint32_t mx = len;
     #pragma unroll
@@ -997,7 +955,7 @@ __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__r
                     eqb += m && kj == key && j < idx;
                 }
                 if (live) {
-                    const uint64_t newbits = (uint64_t)db + adv;
+                    const uint64_t newbits = (uint64_t)db + 64;
                     const bool final_depth = newbits >= 8ull * n;
                     const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
                     if (eqt > 1 && eqb == 0)
@@ -1194,7 +1152,6 @@ __device__ __forceinline__ void sort_seg(const DataArgs &a, const Seg4 sg, uint3
     // the network sorts slots [0, M): threads t < M / E hold them (slot t * E + e); the order
     // inside is free, so the loads are coalesced (element e * R + t of the segment)
     const uint32_t R = M >= E ? M / E : 1u;
-    const CWin cw = cwin_shape(a, b, db);
     uint64_t k[E];
     uint32_t p[E];
 #pragma unroll
@@ -1204,7 +1161,7 @@ __device__ __forceinline__ void sort_seg(const DataArgs &a, const Seg4 sg, uint3
         p[e] = 0xffffffffu;
         if (t < R && i < len) {
             p[e] = a.sa[gstart + i];
-            k[e] = list_window(a, blk, n, b, p[e], db, cw);
+            k[e] = rot_window(blk, n, p[e], db);
         }
     }
     for (uint32_t i = t; i < CAP / 32; i += NT) s_tail[i] = 0;
@@ -1220,7 +1177,7 @@ __device__ __forceinline__ void sort_seg(const DataArgs &a, const Seg4 sg, uint3
     for (uint32_t i = t; i < len; i += NT)
         if (i + 1 == len || s_key[i + 1] != s_key[i]) atomicOr(&s_tail[i >> 5], 1u << (i & 31u));
     sync();
-    const bool final_depth = (uint64_t)db + cwin_adv(cw) >= 8ull * n;
+    const bool final_depth = (uint64_t)db + 64 >= 8ull * n;
 #pragma unroll
     for (uint32_t e = 0; e < E; ++e) {
         const uint32_t i = t + e * NT;
@@ -1250,13 +1207,13 @@ __device__ __forceinline__ void sort_seg(const DataArgs &a, const Seg4 sg, uint3
     }
 }
 
-// the tie runs sort_seg found, deferred one window deeper (64 raw bits, or cwin_adv)
+// the tie runs sort_seg found, deferred 64 bits deeper
 template <uint32_t NT, uint32_t E, uint32_t Q>
 __device__ __forceinline__ void sort_seg_defer(const DataArgs &a, const Seg4 sg, uint32_t t, const uint32_t (&hm)[E],
                                                DeferQueue<Q> &dq)
 {
     const uint32_t n = a.boffs[sg.w + 1] - a.boffs[sg.w];
-    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)sg.z + cwin_adv(cwin_shape(a, sg.w, sg.z)), 0xffffffffull);
+    const uint32_t nd = (uint32_t)min<uint64_t>((uint64_t)sg.z + 64, 0xffffffffull);
 #pragma unroll
     for (uint32_t e = 0; e < E; ++e)
         if (hm[e]) dq_push(a, dq, sg.x + t + e * NT, hm[e], nd, sg.w, n);
