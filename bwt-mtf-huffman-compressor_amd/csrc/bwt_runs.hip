@@ -105,9 +105,9 @@ __global__ __launch_bounds__(256) void k_prim_scatter(const uint32_t *__restrict
 // 256 threads x 16 each.
 constexpr uint32_t kPrimTile = 4096;
 
-// Run heads of one block, in position order (stream compaction of T[p] != T[p - 1], cyclic):
-// per-tile head counts, their exclusive scan (k_tiles_excl), then each thread writes the heads of
-// its 16 consecutive positions at its tile's offset + its workgroup prefix.
+// Run heads in position order (stream compaction of T[p] != T[p - 1], cyclic): per-tile head
+// counts, their exclusive scan (k_tiles_excl), then each thread writes the heads of its 16
+// consecutive positions at its tile's offset + its workgroup prefix (k_bheads_*).
 __device__ __forceinline__ uint32_t head_bits16(const uint8_t *__restrict__ t, uint32_t n, uint32_t p0)
 {
     uint32_t f = 0;
@@ -122,28 +122,6 @@ __device__ __forceinline__ uint32_t head_bits16(const uint8_t *__restrict__ t, u
     }
     return f;
 }
-__global__ __launch_bounds__(256) void k_heads_count(const uint8_t *__restrict__ t, uint32_t n, uint32_t *__restrict__ tcnt)
-{
-    __shared__ uint32_t s_tmp[8];
-    const uint32_t c = (uint32_t)__builtin_popcount(head_bits16(t, n, blockIdx.x * kPrimTile + 16u * threadIdx.x));
-    uint32_t tot;
-    block_excl_sum1<256>(c, s_tmp, &tot);
-    if (threadIdx.x == 0) tcnt[blockIdx.x] = tot;
-}
-__global__ __launch_bounds__(256) void k_heads_write(const uint8_t *__restrict__ t, uint32_t n,
-                                                     const uint32_t *__restrict__ toff, uint32_t *__restrict__ H)
-{
-    __shared__ uint32_t s_tmp[8];
-    const uint32_t p0 = blockIdx.x * kPrimTile + 16u * threadIdx.x;
-    uint32_t f = head_bits16(t, n, p0);
-    uint32_t o = toff[blockIdx.x] + block_excl_sum1<256>((uint32_t)__builtin_popcount(f), s_tmp);
-    while (f) {
-        const uint32_t k = (uint32_t)__builtin_ctz(f);
-        H[o++] = p0 + k;
-        f &= f - 1;
-    }
-}
-
 // One workgroup: exclusive prefix (op = sum, or max with identity 0) of cnt[0..m) into out.
 template <bool MAX>
 __global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict__ cnt, uint32_t m, uint32_t *__restrict__ out)
@@ -300,30 +278,6 @@ __global__ __launch_bounds__(256) void k_rsort_copy(const uint64_t *__restrict__
     }
 }
 
-// K_i = c_i << 25 | [d_i > c_i] << 24 | (d_i > c_i ? ~L_i : L_i) & 0xffffff, value i
-__global__ __launch_bounds__(256) void k_run_keys(const uint8_t *__restrict__ t, uint32_t n, const uint32_t *__restrict__ H,
-                                                  uint32_t m, uint64_t *__restrict__ key, uint32_t *__restrict__ idx)
-{
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t h = H[i], hn = H[i + 1 < m ? i + 1 : 0];
-    const uint32_t len = hn > h ? hn - h : hn + n - h;
-    const uint32_t cc = t[h], d = t[hn], up = d > cc;
-    key[i] = (uint64_t)cc << 25 | (uint64_t)up << 24 | (up ? kMask24 - len : len);
-    idx[i] = i;
-}
-
-// (rank_i, rank_{i+h}) packed in 2 * bits, value i
-__global__ __launch_bounds__(256) void k_pair_keys(const uint32_t *__restrict__ rank, uint32_t m, uint32_t h,
-                                                   uint32_t bits, uint64_t *__restrict__ key, uint32_t *__restrict__ idx)
-{
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t j = i + h < m ? i + h : i + h - m;
-    key[i] = (uint64_t)rank[i] << bits | rank[j];
-    idx[i] = i;
-}
-
 // first sorted slot of each key's group (0 elsewhere) per thread run of 16 slots, the tile's
 // largest (its last head) in tmax, and the group count
 __global__ __launch_bounds__(256) void k_group_heads(const uint64_t *__restrict__ sk, uint32_t m, uint32_t *__restrict__ tmax,
@@ -363,39 +317,125 @@ __global__ __launch_bounds__(256) void k_rank_scatter(const uint64_t *__restrict
     }
 }
 
-// position keys (header comment), value p
-__global__ __launch_bounds__(256) void k_pos_keys(const uint8_t *__restrict__ t, uint32_t n, const uint32_t *__restrict__ H,
-                                                  uint32_t m, const uint32_t *__restrict__ rank, uint64_t *__restrict__ key,
-                                                  uint32_t *__restrict__ val)
+// ---- a batch of run-heavy blocks, sorted together: run j of block b is global run R_b + j,
+// position p of block b is global position P_b + p; the block index sits above every sort key,
+// so one sort (and one host wait a doubling round) serves all of them.
+struct RBlk {
+    uint64_t toff;      // byte offset of the block in the batch (input and L)
+    uint32_t n, m;      // positions, cyclic runs
+    uint32_t R, P, T;   // first global run, position, 4 K tile
+    uint32_t slot;      // index of the block's primary in the output array
+};
+
+// run heads: grid (tiles of kPrimTile positions, blocks)
+__global__ __launch_bounds__(256) void k_bheads_count(const uint8_t *__restrict__ in, const RBlk *__restrict__ tab,
+                                                      uint32_t *__restrict__ tcnt)
 {
+    __shared__ uint32_t s_tmp[8];
+    const RBlk B = tab[blockIdx.y];
+    if (blockIdx.x * kPrimTile >= B.n) return;  // workgroup-uniform
+    const uint32_t c = (uint32_t)__builtin_popcount(head_bits16(in + B.toff, B.n, blockIdx.x * kPrimTile + 16u * threadIdx.x));
+    uint32_t tot;
+    block_excl_sum1<256>(c, s_tmp, &tot);
+    if (threadIdx.x == 0) tcnt[B.T + blockIdx.x] = tot;
+}
+// H[global run] = block-relative head position, rblk[global run] = block (toff: the tiles' exclusive
+// prefix, so block b's heads start at R_b)
+__global__ __launch_bounds__(256) void k_bheads_write(const uint8_t *__restrict__ in, const RBlk *__restrict__ tab,
+                                                      const uint32_t *__restrict__ toff, uint32_t *__restrict__ H,
+                                                      uint32_t *__restrict__ rblk)
+{
+    __shared__ uint32_t s_tmp[8];
+    const RBlk B = tab[blockIdx.y];
+    if (blockIdx.x * kPrimTile >= B.n) return;
+    const uint32_t p0 = blockIdx.x * kPrimTile + 16u * threadIdx.x;
+    uint32_t f = head_bits16(in + B.toff, B.n, p0);
+    uint32_t o = toff[B.T + blockIdx.x] + block_excl_sum1<256>((uint32_t)__builtin_popcount(f), s_tmp);
+    while (f) {
+        const uint32_t k = (uint32_t)__builtin_ctz(f);
+        H[o] = p0 + k;
+        rblk[o++] = blockIdx.y;
+        f &= f - 1;
+    }
+}
+
+// K_i = b << 33 | c_i << 25 | [d_i > c_i] << 24 | (d_i > c_i ? ~L_i : L_i) & 0xffffff, value i
+__global__ __launch_bounds__(256) void k_brun_keys(const uint8_t *__restrict__ in, const RBlk *__restrict__ tab,
+                                                   const uint32_t *__restrict__ H, const uint32_t *__restrict__ rblk,
+                                                   uint32_t M, uint64_t *__restrict__ key, uint32_t *__restrict__ idx)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= M) return;
+    const uint32_t b = rblk[i];
+    const RBlk B = tab[b];
+    const uint8_t *t = in + B.toff;
+    const uint32_t li = i - B.R;
+    const uint32_t h = H[i], hn = H[B.R + (li + 1 < B.m ? li + 1 : 0)];
+    const uint32_t len = hn > h ? hn - h : hn + B.n - h;
+    const uint32_t cc = t[h], d = t[hn], up = d > cc;
+    key[i] = (uint64_t)b << 33 | (uint64_t)cc << 25 | (uint64_t)up << 24 | (up ? kMask24 - len : len);
+    idx[i] = i;
+}
+
+// (rank_i, rank of the run h further on in the same block, cyclic) packed in 2 * bits, value i
+__global__ __launch_bounds__(256) void k_bpair_keys(const RBlk *__restrict__ tab, const uint32_t *__restrict__ rblk,
+                                                    const uint32_t *__restrict__ rank, uint32_t M, uint32_t h, uint32_t bits,
+                                                    uint64_t *__restrict__ key, uint32_t *__restrict__ idx)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= M) return;
+    const RBlk B = tab[rblk[i]];
+    const uint32_t j = B.R + (uint32_t)(((uint64_t)(i - B.R) + h) % B.m);
+    key[i] = (uint64_t)rank[i] << bits | rank[j];
+    idx[i] = i;
+}
+
+// position keys (header comment) below the block index, value p: grid (tiles of 256, blocks)
+__global__ __launch_bounds__(256) void k_bpos_keys(const uint8_t *__restrict__ in, const RBlk *__restrict__ tab,
+                                                   const uint32_t *__restrict__ H, const uint32_t *__restrict__ rank,
+                                                   uint64_t *__restrict__ key, uint32_t *__restrict__ val)
+{
+    const RBlk B = tab[blockIdx.y];
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= n) return;
+    if (p >= B.n) return;
+    if (B.m == 0) {  // one byte value: identical rotations, kept in position order
+        key[B.P + p] = (uint64_t)blockIdx.y << 57 | p;
+        val[B.P + p] = p;
+        return;
+    }
+    const uint8_t *t = in + B.toff;
+    const uint32_t *Hb = H + B.R, m = B.m;
     // run of p: the last head <= p, or the wrapping last run when p precedes H[0]
-    uint32_t lo = 0, hi = m;  // H[lo] <= p < H[hi] (H[m] = infinity)
-    if (p < H[0]) {
+    uint32_t lo = 0, hi = m;  // Hb[lo] <= p < Hb[hi] (Hb[m] = infinity)
+    if (p < Hb[0]) {
         lo = m - 1;
     } else {
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (H[mid] <= p) lo = mid;
+            if (Hb[mid] <= p) lo = mid;
             else hi = mid;
         }
     }
-    const uint32_t nx = lo + 1 < m ? lo + 1 : 0, hn = H[nx];
-    const uint32_t r = hn > p ? hn - p : hn + n - p;
+    const uint32_t nx = lo + 1 < m ? lo + 1 : 0, hn = Hb[nx];
+    const uint32_t r = hn > p ? hn - p : hn + B.n - p;
     const uint32_t cc = t[p], up = t[hn] > cc;
-    key[p] = (uint64_t)cc << 49 | (uint64_t)up << 48 | (uint64_t)(up ? kMask24 - r : r) << 24 | rank[nx];
-    val[p] = p;
+    key[B.P + p] = (uint64_t)blockIdx.y << 57 | (uint64_t)cc << 49 | (uint64_t)up << 48 |
+                   (uint64_t)(up ? kMask24 - r : r) << 24 | rank[B.R + nx];
+    val[B.P + p] = p;
 }
 
-__global__ __launch_bounds__(256) void k_run_out(const uint8_t *__restrict__ t, uint32_t n, const uint32_t *__restrict__ sp,
-                                                 uint8_t *__restrict__ L, uint32_t *__restrict__ prim)
+// L and primaries from the sorted positions: grid (tiles of 256, blocks)
+__global__ __launch_bounds__(256) void k_brun_out(const uint8_t *__restrict__ in, const RBlk *__restrict__ tab,
+                                                  const uint32_t *__restrict__ sp, uint8_t *__restrict__ L,
+                                                  uint32_t *__restrict__ prim)
 {
+    const RBlk B = tab[blockIdx.y];
     const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t p = sp ? sp[j] : j;
-    L[j] = t[p ? p - 1 : n - 1];
-    if (p == 0) *prim = j;
+    if (j >= B.n) return;
+    const uint8_t *t = in + B.toff;
+    const uint32_t p = B.m ? sp[B.P + j] : j;  // one byte value: n identical rotations in order
+    L[B.toff + j] = t[p ? p - 1 : B.n - 1];
+    if (p == 0) prim[B.slot] = j;
 }
 
 inline uint32_t bits_for(uint32_t v)  // bits holding 0 .. v
@@ -406,25 +446,27 @@ inline uint32_t bits_for(uint32_t v)  // bits holding 0 .. v
 }
 
 struct RunWs {
-    uint32_t *H, *idx, *idx2, *rank, *cnt, *tcnt, *toff, *rowpre, *dtot;
+    uint32_t *H, *rblk, *idx, *idx2, *rank, *cnt, *tcnt, *toff, *rowpre, *dtot;
     uint64_t *key, *key2;
     uint64_t *pkey, *pkey2;
     uint32_t *pval, *pval2;
+    RBlk *tab;
 };
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Workspace of one block's run BWT (n positions, m runs), carved from one slot.
-RunWs run_ws(Ctx *c, uint32_t n, uint32_t m)
+// Workspace of a run batch (N positions, M runs, NT position tiles, B blocks), carved from one slot.
+RunWs run_ws(Ctx *c, uint64_t N, uint32_t M, uint32_t NT, uint32_t B)
 {
-    const size_t mm = std::max(m, 1u), nt = cdiv(std::max(n, 1u), kPrimTile);
-    const size_t sizes[] = {align256(mm * 4) * 4 + 256, align256(nt * 4) * 2, align256(kRsBins * nt * 4) + kRsBins * 4,
-                            align256(mm * 8) * 2, align256((size_t)n * 8) * 2, align256((size_t)n * 4) * 2};
+    const size_t mm = std::max(M, 1u), nt = std::max<size_t>(NT, cdiv(std::max<uint64_t>(N, 1), kRsTile));
+    const size_t sizes[] = {align256(mm * 4) * 5 + 256, align256(nt * 4) * 2, align256(kRsBins * nt * 4) + kRsBins * 4,
+                            align256(mm * 8) * 2, align256((size_t)N * 8) * 2, align256((size_t)N * 4) * 2,
+                            align256((size_t)B * sizeof(RBlk))};
     size_t total = 0;
     for (size_t z : sizes) total += z;
     uint8_t *p = (uint8_t *)c->get(WS_RUNS, total);
     RunWs w;
-    uint32_t **u32s[] = {&w.H, &w.idx, &w.idx2, &w.rank};
+    uint32_t **u32s[] = {&w.H, &w.rblk, &w.idx, &w.idx2, &w.rank};
     for (auto q : u32s) {
         *q = (uint32_t *)p;
         p += align256(mm * 4);
@@ -444,12 +486,14 @@ RunWs run_ws(Ctx *c, uint32_t n, uint32_t m)
     w.key2 = (uint64_t *)p;
     p += align256(mm * 8);
     w.pkey = (uint64_t *)p;
-    p += align256((size_t)n * 8);
+    p += align256((size_t)N * 8);
     w.pkey2 = (uint64_t *)p;
-    p += align256((size_t)n * 8);
+    p += align256((size_t)N * 8);
     w.pval = (uint32_t *)p;
-    p += align256((size_t)n * 4);
+    p += align256((size_t)N * 4);
     w.pval2 = (uint32_t *)p;
+    p += align256((size_t)N * 4);
+    w.tab = (RBlk *)p;
     return w;
 }
 
@@ -492,32 +536,52 @@ void sort_pairs(Ctx *c, RunWs &w, uint64_t *kin, uint64_t *kout, uint32_t *vin, 
     if (ks != kout) BMH_LAUNCH(c, "bwt_run_sort", k_rsort_copy, cdiv(cnt, 256), 256, 0, ks, vs, kout, vout, cnt);
 }
 
-// The BWT of one run-heavy block t[0..n) with m >= 0 cyclic runs: L[0..n) and *prim (device).
-void run_block(Ctx *c, const uint8_t *t, uint32_t n, uint32_t m, uint8_t *L, uint32_t *prim, uint32_t *h_cnt)
+// The BWT of run-heavy blocks, all at once: block i = bytes [offs[i], offs[i] + ns[i]) of the
+// batch `in` with ms[i] >= 0 cyclic runs; L at the same offsets of `L`, primary i in prim[i]
+// (device). At most kRunBatchBlocks blocks (the block index takes the top bits of the keys).
+constexpr uint32_t kRunBatchBlocks = 128;
+void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &offs, const std::vector<uint32_t> &ns,
+                      const std::vector<uint32_t> &ms, uint8_t *L, uint32_t *prim, uint32_t *h_cnt)
 {
-    if (m == 0) {  // one byte value: n identical rotations
-        BMH_LAUNCH(c, "bwt_run_out", k_run_out, cdiv(n, 256), 256, 0, t, n, (const uint32_t *)nullptr, L, prim);
-        return;
+    const uint32_t B = (uint32_t)offs.size();
+    if (B == 0) return;
+    if (B > kRunBatchBlocks) fail(BMH_EINVAL, "bwt: too many run blocks in one batch");
+    std::vector<RBlk> tab(B);
+    uint64_t N = 0;
+    uint32_t M = 0, NT = 0, maxn = 0, maxm = 0;
+    for (uint32_t i = 0; i < B; ++i) {
+        tab[i] = RBlk{offs[i], ns[i], ms[i], M, (uint32_t)N, NT, i};
+        N += ns[i];
+        M += ms[i];
+        NT += cdiv(ns[i], kPrimTile);
+        maxn = std::max(maxn, ns[i]);
+        maxm = std::max(maxm, ms[i]);
     }
-    RunWs w = run_ws(c, n, m);
-    const uint32_t ntn = cdiv(n, kPrimTile);
-    BMH_LAUNCH(c, "bwt_run_heads", k_heads_count, ntn, 256, 0, t, n, w.tcnt);
-    BMH_LAUNCH(c, "bwt_run_heads", k_tiles_excl<false>, 1, 1024, 0, w.tcnt, ntn, w.toff);
-    BMH_LAUNCH(c, "bwt_run_heads", k_heads_write, ntn, 256, 0, t, n, w.toff, w.H);
-    BMH_LAUNCH(c, "bwt_run_keys", k_run_keys, cdiv(m, 256), 256, 0, t, n, w.H, m, w.key, w.idx);
-    sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, m, 33);
-    uint32_t groups = rank_groups(c, w, w.key2, w.idx2, m, h_cnt);
-    const uint32_t bits = bits_for(m - 1);
-    for (uint64_t h = 1; groups < m && h < m; h *= 2) {
-        BMH_LAUNCH(c, "bwt_run_keys", k_pair_keys, cdiv(m, 256), 256, 0, w.rank, m, (uint32_t)h, bits, w.key, w.idx);
-        sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, m, 2 * bits);
-        groups = rank_groups(c, w, w.key2, w.idx2, m, h_cnt);
+    RunWs w = run_ws(c, N, M, NT, B);
+    c->h2d(w.tab, tab.data(), (size_t)B * sizeof(RBlk));
+    const uint32_t bb = bits_for(B - 1);
+    if (M > 0) {
+        const dim3 tgrid(cdiv(maxn, kPrimTile), B);
+        BMH_HIP(hipMemsetAsync(w.tcnt, 0, (size_t)NT * 4, c->stream));
+        BMH_LAUNCH(c, "bwt_run_heads", k_bheads_count, tgrid, 256, 0, in, w.tab, w.tcnt);
+        BMH_LAUNCH(c, "bwt_run_heads", k_tiles_excl<false>, 1, 1024, 0, w.tcnt, NT, w.toff);
+        BMH_LAUNCH(c, "bwt_run_heads", k_bheads_write, tgrid, 256, 0, in, w.tab, w.toff, w.H, w.rblk);
+        BMH_LAUNCH(c, "bwt_run_keys", k_brun_keys, cdiv(M, 256), 256, 0, in, w.tab, w.H, w.rblk, M, w.key, w.idx);
+        sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 33 + bb);
+        uint32_t groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
+        const uint32_t bits = bits_for(M - 1);
+        for (uint64_t h = 1; groups < M && h < maxm; h *= 2) {
+            BMH_LAUNCH(c, "bwt_run_keys", k_bpair_keys, cdiv(M, 256), 256, 0, w.tab, w.rblk, w.rank, M, (uint32_t)h, bits,
+                       w.key, w.idx);
+            sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 2 * bits);
+            groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
+        }
+        const dim3 pgrid(cdiv(maxn, 256), B);
+        BMH_LAUNCH(c, "bwt_run_place", k_bpos_keys, pgrid, 256, 0, in, w.tab, w.H, w.rank, w.pkey, w.pval);
+        sort_pairs(c, w, w.pkey, w.pkey2, w.pval, w.pval2, (uint32_t)N, 57 + bb);
     }
-    BMH_LAUNCH(c, "bwt_run_place", k_pos_keys, cdiv(n, 256), 256, 0, t, n, w.H, m, w.rank, w.pkey, w.pval);
-    sort_pairs(c, w, w.pkey, w.pkey2, w.pval, w.pval2, n, 57);
-    BMH_LAUNCH(c, "bwt_run_out", k_run_out, cdiv(n, 256), 256, 0, t, n, w.pval2, L, prim);
+    BMH_LAUNCH(c, "bwt_run_out", k_brun_out, dim3(cdiv(maxn, 256), B), 256, 0, in, w.tab, w.pval2, L, prim);
 }
-
 }  // namespace
 
 // Batch BWT: small batches are screened for run-heavy blocks, which take the run path above;
@@ -566,9 +630,17 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         WallPhase wall(x, "bwt_runs");
         uint32_t *p = (uint32_t *)x->get(WS_RUN_PRIM, rb.size() * 4 + 64);
         uint32_t h_cnt = 0;
-        for (size_t i = 0; i < rb.size(); ++i) {
-            const uint64_t o = bt.offs[rb[i]];
-            run_block(x, d_in + o, (uint32_t)(bt.offs[rb[i] + 1] - o), runs[rb[i]], d_L + o, p + i, &h_cnt);
+        // all run blocks sorted together (one host wait a doubling round for all of them), in
+        // groups of at most kRunBatchBlocks
+        for (size_t g = 0; g < rb.size(); g += kRunBatchBlocks) {
+            std::vector<uint64_t> offs;
+            std::vector<uint32_t> ns, ms;
+            for (size_t i = g; i < std::min(rb.size(), g + kRunBatchBlocks); ++i) {
+                offs.push_back(bt.offs[rb[i]]);
+                ns.push_back((uint32_t)(bt.offs[rb[i] + 1] - bt.offs[rb[i]]));
+                ms.push_back(runs[rb[i]]);
+            }
+            run_blocks_batch(x, d_in, offs, ns, ms, d_L, p + g, &h_cnt);
         }
         rp = p;
     };

@@ -98,6 +98,39 @@ def test_run_blocks_in_mixed_batches(ctx, oracle):
             assert rec == oracle.encode(blk), [len(b) for b in lay]
 
 
+def test_run_blocks_sorted_together(ctx, oracle):
+    """Every run shape in one batch (run blocks only, then with sorter blocks between): the run
+    path sorts all of a batch's run blocks together (block index above every key, one host wait
+    a doubling round for all), one-value blocks included. BWT and records equal the oracle's."""
+    blocks = [RUN_CASES[k]() for k in sorted(RUN_CASES)]
+    blocks += [sparse_bitmap(21, 262_144), sparse_bitmap(22, 251_072)]  # Calgary pic's 256 KiB halves' shape
+    offs = np.cumsum([0] + [len(b) for b in blocks]).astype(np.uint64)
+    d_in, d_L = ctx.alloc(int(offs[-1])), ctx.alloc(int(offs[-1]))
+    d_in.upload(np.frombuffer(b"".join(blocks), np.uint8))
+    ctx.reset_stats()
+    ctx.set_timing(True)
+    prim = ctx.bwt_dev(d_in, offs, d_L)
+    st = ctx.kernel_stats()
+    ctx.set_timing(False)
+    L = d_L.download()
+    d_in.free()
+    d_L.free()
+    assert "bwt_g1_scatter" not in st, sorted(st)
+    for i, b in enumerate(blocks):
+        op, oL = oracle.bwt(b)
+        assert int(prim[i]) == op and L[int(offs[i]):int(offs[i + 1])].tobytes() == oL, (i, len(b))
+    # sorter blocks between them, past kBandCeil (128 KiB) so the oracle's closed-form Huffman
+    # tie-break is the reference's (below it the reference follows its heap history, which
+    # heap_order.cpp replays and tests/test_bands.py pins against the reference's own records)
+    rng = np.random.default_rng(3)
+    mixed = []
+    for b in blocks[:6]:
+        mixed += [b, rng.integers(0, 30, 140_000).astype(np.uint8).tobytes()]
+    recs = ctx.encode_blocks(mixed)
+    for blk, rec in zip(mixed, recs):
+        assert rec == oracle.encode(blk)
+
+
 def test_run_path_compress_roundtrip(ctx):
     """compress_bytes over a run-heavy stream (blocks cut at 1 MiB, batches <= 64 MiB are
     screened) round-trips and matches the single-block-per-call records."""
