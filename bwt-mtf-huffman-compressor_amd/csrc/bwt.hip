@@ -62,8 +62,11 @@ constexpr uint64_t kMergeSortBatch = 16ull << 20;   // ... and launch two bitoni
 static_assert(kFinCap <= kBigCapLarge && kBigCapLarge <= kSegCap && kSegCap <= kDenseCap, "list classes");
 constexpr uint32_t kSmallM = 64;                // sub-bucket size sorted by rank counting
 constexpr uint32_t kTinyFin = 64;               // list segments this small: one wave each
-constexpr uint32_t kDataMaxBits = 512;          // deeper MSD ties go to rank doubling
-constexpr uint32_t kFinMaxBits = 512;           // deeper finish-pass ties go to rank doubling
+// Ties deeper than this go to rank doubling (DataArgs::dbl_bits): 512 bits in large batches,
+// 256 in the latency-bound ones that store the full suffix array from the start (no data-phase
+// re-run): Calgary 3.0 -> 2.8-2.9 ms whole files, 2.8 -> 2.6 ms at 256 KiB; Zipf text at 256
+// would re-run large batches' data phase (100 MB: 10.0 -> 12.9 ms).
+constexpr uint32_t kDblBitsLarge = 512, kDblBitsSmall = 256;
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
 constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries per workgroup
 #ifndef BMH_TINY_Q
@@ -162,6 +165,7 @@ struct DataArgs {
     const uint8_t *arank;   // per block: 256-entry byte -> rank map of a compacted alphabet
     uint32_t full_sa;  // 0: SA only for slots a later pass reads (deferred / tied / MSD)
     uint32_t big_cap;  // list segments longer than this take MSD passes (kBigCapLarge / kBigCapSmall)
+    uint32_t dbl_bits; // tied segments this deep go to rank doubling (kDblBitsLarge / kDblBitsSmall)
 };
 
 __device__ __forceinline__ uint8_t lastcol_byte(const uint8_t *blk, uint32_t n, uint32_t p)
@@ -234,7 +238,7 @@ __device__ __forceinline__ uint32_t defer_list(const DataArgs &a, Seg4 &sg, uint
         sg.w |= kFinalFlag;
         return kListGroups;
     }
-    if (sg.z >= kFinMaxBits) {
+    if (sg.z >= a.dbl_bits) {
         a.bflag[sg.w] = 1;
         a.cnt->flagged = 1;
         return kListGroups;
@@ -1499,7 +1503,7 @@ __device__ __forceinline__ void dscan_one(const DataArgs &a, const Seg4 *__restr
     __syncthreads();
     auto route = [&](uint32_t gs, uint32_t len) {
         if (len == 1) return;  // resolved by the scatter
-        if (final_depth || nd >= kDataMaxBits) {
+        if (final_depth || nd >= a.dbl_bits) {
             if (!final_depth) {
                 a.bflag[b] = 1;
                 a.cnt->flagged = 1;
@@ -2401,6 +2405,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     for (;;) {
         da.full_sa = full_sa ? 1u : 0u;
         da.big_cap = big_cap;
+        da.dbl_bits = N <= kFullSaBatch ? kDblBitsSmall : kDblBitsLarge;
         if (kb_cur != rec) std::swap(kb_cur, kb_nxt);  // the global pass writes its windows into rec
         static_assert(sizeof(Counters) % 4 == 0, "counter words");
         constexpr uint32_t kCntWords = sizeof(Counters) / 4;
