@@ -470,7 +470,7 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
                                                   const uint8_t *__restrict__ arank, uint32_t *__restrict__ bits,
                                                   uint32_t recount)  // bits: 8 words a chunk
 {
-    __shared__ uint32_t h[4][kG1Bins];
+    __shared__ __align__(16) uint32_t h[4][kG1Bins];
     __shared__ uint8_t s_rk[256];
     const uint32_t t = threadIdx.x, w = (t >> 6) & 3u;
     uint32_t *const rcount = rlist - 1;  // rlist[-1] = its length, zeroed by the raw pass
@@ -511,12 +511,16 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
         chist[(size_t)ci * kG1Bins + t] = sum;
         if (!recount) {
             // the chunk's bytes: byte v is present iff one of the digits 4v .. 4v + 3 is counted
+            // (read from the four waves' partial counts: no further barrier)
             static_assert(kG1Bits == 10, "census: 4 raw digits per first byte");
-            __syncthreads();
-            h[0][t] = sum;
-            __syncthreads();
             if (t < 256) {
-                const bool present = (h[0][4 * t] | h[0][4 * t + 1] | h[0][4 * t + 2] | h[0][4 * t + 3]) != 0;
+                uint32_t any = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint4 v = *(const uint4 *)&h[q][4 * t];
+                    any |= v.x | v.y | v.z | v.w;
+                }
+                const bool present = any != 0;
                 const uint64_t bal = __ballot(present);
                 const uint32_t l = t & 63u;
                 if (l < 2) bits[(size_t)ci * 8 + 2 * (t >> 6) + l] = (uint32_t)(bal >> (32 * l));
