@@ -551,19 +551,25 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
 // by it). The pack-chunk histograms say in which chunk each value first appears (value v:
 // the first chunk with a nonzero count, found 16 chunks per step); only those chunks are
 // scanned (on random data: the block's first chunk alone), one wave per distinct chunk. A value
-// has one first chunk, so the chunks are independent and need no order (a block whose values
-// first appear in 256 different chunks — Calgary pic — scans them 16 at a time).
-constexpr uint32_t kFirstNT = 1024;
+// has one first chunk, so the chunks are independent and need no order. Grid (blocks,
+// kFirstWG): every workgroup of a block derives the same sorted list of distinct first chunks
+// (a bitmap over the block's chunks) and scans entries k = 16 g + wave (mod 16 kFirstWG), so a
+// block whose values first appear in many chunks (Calgary's text files, pic: 100-256) scans
+// them kFirstWG times wider; the one workgroup that scans a value's chunk writes its position.
+constexpr uint32_t kFirstNT = 1024, kFirstWG = 8, kFirstBmWords = 256;  // bitmap: blocks of <= 8192 chunks
 __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restrict__ in, const uint32_t *__restrict__ boffs,
                                                         const uint32_t *__restrict__ pfirst,
                                                         const uint32_t *__restrict__ freq,
                                                         const uint16_t *__restrict__ chist, uint32_t *__restrict__ first)
 {
-    __shared__ uint32_t f[256], s_cv[256], s_list[256], s_nlist;
-    const uint32_t b = blockIdx.x, t = threadIdx.x, w = t >> 6, l = t & 63u;
+    __shared__ uint32_t f[256], s_cv[256], s_list[256], s_nlist, s_bm[kFirstBmWords], s_tmp[kFirstNT / 64 + 1];
+    const uint32_t b = blockIdx.x, g = blockIdx.y, t = threadIdx.x, w = t >> 6, l = t & 63u;
     const uint32_t c0 = pfirst[b], nc = pfirst[b + 1] - c0;
     const uint32_t o = boffs[b], n = boffs[b + 1] - o;
+    const bool bitmap = nc <= 32 * kFirstBmWords;  // else workgroup 0 alone, leads by value order
+    if (!bitmap && g != 0) return;                 // workgroup-uniform
     if (t == 0) s_nlist = 0;
+    if (t < kFirstBmWords) s_bm[t] = 0;
     if (t < 256) {
         f[t] = 0xffffffffu;
         uint32_t cv = 0xffffffffu;  // first chunk holding t (block-relative); none for absent values
@@ -580,7 +586,17 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
         s_cv[t] = cv;
     }
     __syncthreads();
-    if (t < 256) {  // the smallest value of each distinct first chunk lists it
+    if (bitmap) {
+        if (t < 256 && s_cv[t] != 0xffffffffu) atomicOr(&s_bm[s_cv[t] >> 5], 1u << (s_cv[t] & 31u));
+        __syncthreads();
+        // the distinct first chunks in increasing order (the same list in every workgroup)
+        uint32_t bits = t < kFirstBmWords ? s_bm[t] : 0u;
+        uint32_t pos = block_excl_sum1<kFirstNT>((uint32_t)__builtin_popcount(bits), s_tmp, &s_nlist);
+        while (bits) {
+            s_list[pos++] = 32 * t + (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
+        }
+    } else if (t < 256) {  // the smallest value of each distinct first chunk lists it
         const uint32_t cv = s_cv[t];
         bool lead = cv != 0xffffffffu;
         for (uint32_t u = 0; u < t && lead; ++u) lead = s_cv[u] != cv;
@@ -588,8 +604,9 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
     }
     __syncthreads();
     const uint32_t nl = s_nlist;
+    const uint32_t k0 = bitmap ? 16 * g + w : w, kstep = bitmap ? 16 * kFirstWG : kFirstNT / 64;
     static_assert(kPackChunkSyms == 64 * 64, "k_mtf_first: a wave's 64 lanes x 64 symbols cover one pack chunk");
-    for (uint32_t k = w; k < nl; k += kFirstNT / 64) {  // lane l: symbols [64l, 64l + 64) of the chunk
+    for (uint32_t k = k0; k < nl; k += kstep) {  // lane l: symbols [64l, 64l + 64) of the chunk
         const uint32_t cm = s_list[k], p0 = cm * kPackChunkSyms, len = min(kPackChunkSyms, n - p0);
         const uint32_t e0 = 64 * l;
         uint32_t sw[16];
@@ -622,7 +639,8 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
         }
     }
     __syncthreads();
-    if (t < 256) first[(size_t)b * 256 + t] = f[t];
+    // each present value's first chunk was scanned by exactly one workgroup; absent values by 0
+    if (t < 256 && (f[t] != 0xffffffffu || (g == 0 && s_cv[t] == 0xffffffffu))) first[(size_t)b * 256 + t] = f[t];
 }
 
 }  // namespace
@@ -742,7 +760,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
     BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist);
-    BMH_LAUNCH(c, "mtf_first", k_mtf_first, nb, kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist, d_first);
+    BMH_LAUNCH(c, "mtf_first", k_mtf_first, dim3(nb, kFirstWG), kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist,
+               d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
     if (h_freq32 || h_first32) c->sync();
