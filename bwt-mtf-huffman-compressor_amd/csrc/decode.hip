@@ -297,20 +297,21 @@ __global__ __launch_bounds__(64) void k_hd_chain(const DBlock *__restrict__ blks
 #pragma unroll
         for (uint32_t j = 0; j < kChainAhead; ++j) {
             const uint32_t k = k0 + j;
-            if (k >= B.nseg) break;
-            const uint64_t s0 = (uint64_t)k * kSegBits;
-            const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
-            uint32_t o = (uint32_t)(T - s0);
-            if (o >= P) {  // cannot happen for a well-formed table; keep the walk in range
-                if (lane == 0) atomicOr(status, 1u);
-                o = 0;
+            if (k < B.nseg) {  // (a guard, not a break: the loop stays unrolled, e[] in registers)
+                const uint64_t s0 = (uint64_t)k * kSegBits;
+                const uint64_t stop = min(s0 + kSegBits, B.pay_bits);
+                uint32_t o = (uint32_t)(T - s0);
+                if (o >= P) {  // cannot happen for a well-formed table; keep the walk in range
+                    if (lane == 0) atomicOr(status, 1u);
+                    o = 0;
+                }
+                const uint32_t v = __shfl(e[j], (int)o, 64);
+                if (lane == 0) {
+                    seg_start[B.seg0 + k] = T;
+                    seg_cnt[B.seg0 + k] = v >> 8;
+                }
+                T = stop + (v & 255u);
             }
-            const uint32_t v = __shfl(e[j], (int)o, 64);
-            if (lane == 0) {
-                seg_start[B.seg0 + k] = T;
-                seg_cnt[B.seg0 + k] = v >> 8;
-            }
-            T = stop + (v & 255u);
         }
     }
 }
