@@ -144,24 +144,20 @@ class DeviceEncoder:
         return [a[int(self.ro[i]):int(self.ro[i + 1])] for i in range(len(self.mine))]
 
 
-def kernel_leg(enc: DeviceEncoder, ksteps: int) -> tuple[dict, dict]:
+def kernel_leg(enc: DeviceEncoder, ksteps: int, pipelines: int = 0) -> tuple[dict, dict]:
     """A separate pass with HIP events around every launch on the context stream. The timed
     region splits each batch over several pipelines (`streams_per_gpu`: kernels overlap,
     stretching their individual durations); this pass runs one stream so each kernel's duration
     is its own."""
     ctx = enc.ctx
-    streams_env = os.environ.get("BMH_STREAMS")
-    os.environ["BMH_STREAMS"] = "1"
+    ctx.set_option("pipelines", 1)
     ctx.reset_stats()
     ctx.set_timing(True)
     for _ in range(ksteps):
         enc.step()
     stats = ctx.kernel_stats()
     ctx.set_timing(False)
-    if streams_env is None:
-        del os.environ["BMH_STREAMS"]
-    else:
-        os.environ["BMH_STREAMS"] = streams_env
+    ctx.set_option("pipelines", pipelines)
     walls = {k[5:]: v for k, v in stats.items() if k.startswith("wall:")}
     stats = {k: v for k, v in stats.items() if not k.startswith("wall:")}
     return stats, walls
@@ -231,7 +227,7 @@ def pcie_leg(r: dist.Rank, enc: DeviceEncoder, steps: int, warmup: int) -> dict:
             "graded_roofline_frac": round(mbs / 1e3 / (r.world * HBM_PEAK_GBS), 6),
             "records_equal_device_encode": bool(ok),
             "rank0_step_ms": [round(x, 2) for x in each[warmup:]],
-            "stream_batch_bytes": int(os.environ.get("BMH_STREAM_BATCH", 256 << 20))}
+            "stream_batch_bytes": 256 << 20}
 
 
 def calgary_leg(ctx: bmh.Context, steps: int) -> dict:
@@ -369,6 +365,10 @@ def main() -> None:
     ap.add_argument("--decode-steps", type=int, default=3, help="timed GPU decode steps of the same records (0: skip)")
     ap.add_argument("--pcie-steps", type=int, default=3, help="timed host-buffer steps (0: skip)")
     ap.add_argument("--calgary-steps", type=int, default=10, help="timed Calgary steps (0: skip)")
+    ap.add_argument("--pipelines", type=int, default=0,
+                    help="pipelines (streams) per device batch for every leg (0: the library's rule; experiments)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="bmh_ctx_set_option for experiments (bmh.Context.OPTIONS), e.g. mtf_chunk=2048")
     a = ap.parse_args()
 
     # control plane over gloo (barriers + scalar reductions only, bmh/dist.py); ranks map to
@@ -379,6 +379,11 @@ def main() -> None:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     dev = r.local_rank % max(1, int(bmh.lib().bmh_device_count()))
     ctx = bmh.Context(dev)
+    if a.pipelines:
+        ctx.set_option("pipelines", a.pipelines)
+    for o in a.opt:
+        k, v = o.split("=", 1)
+        ctx.set_option(k, int(v))
     bs = a.block_size
     mine = rank_plan(r.rank, world, bs, a.scaling, a.bytes_per_gpu, a.total_bytes)
     enc = DeviceEncoder(ctx, mine, bs)
@@ -399,7 +404,7 @@ def main() -> None:
         wenc.d_in.free()
         wenc.d_out.free()
     ksteps = max(1, min(a.steps, 5))
-    stats, walls = kernel_leg(enc, ksteps)
+    stats, walls = kernel_leg(enc, ksteps, a.pipelines)
     recs = enc.records()
     parity = parity_leg(r, recs, mine, bs)
 
@@ -461,10 +466,9 @@ def main() -> None:
             "parity": parity,
             "decode": dec,
         }
-        if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(bs, a.cpu_procs or None)
-        else:
-            line["cpu_baseline"] = None
+        # rank 0 times the reference CPU path after every timed leg, at any world size (the
+        # other ranks have left their legs: nothing else runs on the box's cores or GPUs)
+        line["cpu_baseline"] = None if a.no_cpu_baseline else cpu_baseline(bs, a.cpu_procs or None)
         print(json.dumps(line), flush=True)
     ctx.close()
     dist.finalize(r)

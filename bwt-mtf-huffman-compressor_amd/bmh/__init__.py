@@ -88,6 +88,7 @@ _SIGS = {
     "bmh_container_info": (C.c_int, [P, U64, PU64, PU64]),
     "bmh_container_record": (C.c_int, [P, U64, U64, C.POINTER(P), PU64]),
     "bmh_ctx_set_timing": (C.c_int, [P, C.c_int]),
+    "bmh_ctx_set_option": (C.c_int, [P, U32, U64]),
     "bmh_ctx_reset_stats": (C.c_int, [P]),
     "bmh_ctx_kernel_stats": (C.c_int, [P, P, PU64, C.POINTER(C.c_double), C.c_int]),
     "bmh_synth_splitmix64_dev": (C.c_int, [P, P, U64, U64, U64]),
@@ -240,6 +241,19 @@ class Context:
     def pipelines(self, total: int, nblocks: int) -> int:
         """Pipelines (streams) the library runs a device batch of this shape on."""
         return int(lib().bmh_encode_pipelines(self.h, total, nblocks))
+
+    # ---- tuning options (include/bmh.h BMH_OPT_*; 0 restores the library's rule)
+    OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5}
+
+    def set_option(self, name: str, value: int) -> None:
+        _check(lib().bmh_ctx_set_option(self.h, self.OPTIONS[name], int(value)), f"set_option({name})")
+
+    def set_options(self, spec: str) -> None:
+        """Options from a "name=value,name=value" string (experiment tools pass theirs this way;
+        the library itself reads no environment)."""
+        for item in filter(None, (x.strip() for x in (spec or "").split(","))):
+            k, v = item.split("=", 1)
+            self.set_option(k.strip(), int(v))
 
     # ---- measurement
     def set_timing(self, on: bool) -> None:

@@ -95,7 +95,11 @@ struct Ctx {
     // BWT of a batch's run-heavy blocks runs there beside the rotation sorter (bwt_runs.hip)
     hipStream_t aux_stream = nullptr;
     Ctx *aux = nullptr;
-    int nstreams = 0;  // 0: BMH_STREAMS or the default
+    // tuning options (bmh_ctx_set_option; 0 = the library's rule); sub-pipelines and the side
+    // context copy their parent's at every call
+    struct Options {
+        uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0;
+    } opt;
     // size of the batch a sub-pipeline's sub-batch was cut from (0: its own batch): the run
     // screen is decided on it, so a batch past the screen never sends its sub-batches' run-heavy
     // blocks to the side stream D, which a fourth pipeline holds (bwt_runs.hip)

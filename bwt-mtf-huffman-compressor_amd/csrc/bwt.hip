@@ -69,16 +69,10 @@ constexpr uint32_t kTinyFin = 64;               // list segments this small: one
 constexpr uint32_t kDblBitsLarge = 512, kDblBitsSmall = 256;
 constexpr uint32_t kDTile = 4096;               // MSD / large-path tile
 constexpr uint32_t kDeferQ = 256;               // LDS deferral queue entries per workgroup
-#ifndef BMH_TINY_Q
-#define BMH_TINY_Q 256
-#endif
-constexpr uint32_t kTinyQ = BMH_TINY_Q;        // the packed tiny finish (256 segments per workgroup)
+constexpr uint32_t kTinyQ = 256;               // the packed tiny finish (256 segments per workgroup)
 // doubling phase
 constexpr uint32_t kTinyMax = 64;     // doubling-phase segments ranked by wave shuffles (k_dtiny)
-#ifndef BMH_TINY_EPW
-#define BMH_TINY_EPW 16
-#endif
-constexpr uint32_t kTinyEpwShort = BMH_TINY_EPW;  // tiny-list entries per wave for short lists
+constexpr uint32_t kTinyEpwShort = 16;           // tiny-list entries per wave for short lists
 constexpr uint32_t kTinyWideList = 1u << 17;      // lists this long keep 64 entries per wave
 constexpr uint32_t kDblGrid = 1024;   // fixed grid of the doubling-phase kernels (counts read on the device)
 constexpr uint32_t kMedMax = 4096;
@@ -95,10 +89,8 @@ constexpr uint32_t kRunMode = 1u << 30;
 // window shifted past the bits that pass consumed (K = parent K - consumed). The pass digit
 // starts at most K - kMsdBits bits in, inside the known bits; a segment sharing all of them then
 // has one digit, stays in place and goes on in run mode with gathered windows.
-#ifndef BMH_MSD_BITS
-#define BMH_MSD_BITS 8
-#endif
-constexpr uint32_t kMsdBits = BMH_MSD_BITS, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
+// (10-bit digits measured slower on Zipf text: DESIGN.md §9)
+constexpr uint32_t kMsdBits = 8, kMsdBins = 1u << kMsdBits;  // MSD pass digit; one thread per bin
 static_assert(kMsdBins >= 65 && kMsdBins <= 1024, "MSD digit (run-mode digits 0..64)");
 constexpr uint32_t kWinShift = 16;
 __device__ __forceinline__ uint32_t seg_known(uint32_t w) { return (w >> kWinShift) & 127u; }
@@ -2394,7 +2386,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     // data-phase MSD tiles (built on the device, k_tiles): the big list's slots over kDTile plus
     // one partial tile per segment
     const size_t bcap = ccap[kListBig], dtcap = N / kDTile + bcap + 2;
-    static const bool dbg_lists = getenv("BMH_DBG_LISTS") != nullptr;
+    const bool dbg_lists = c->opt.check_lists != 0;  // BMH_OPT_CHECK_LISTS
     // bitonic list classes merged into two launches per round for latency-bound batches
     const bool merge_sort_classes = N <= kMergeSortBatch;
 

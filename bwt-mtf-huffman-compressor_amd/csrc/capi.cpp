@@ -221,7 +221,7 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
 // next to its copies (C, D). Streams made on demand instead put a third pipeline on pipeline
 // 0's queue when the copy streams came first (Calgary 4.4 -> 7.3 ms), or the D2H copies behind a
 // pipeline when it came first (PCIe-inclusive 30 -> 47-59 ms per GiB); per-call streams paid a
-// queue set-up each call (Calgary 8.5 ms). Pipelines past 3 (BMH_STREAMS) get streams of their
+// queue set-up each call (Calgary 8.5 ms). Pipelines past 3 (BMH_OPT_PIPELINES) get streams of their
 // own and share queues.
 static Ctx *new_sub(Ctx *c, hipStream_t borrowed)
 {
@@ -261,16 +261,18 @@ Ctx *aux_ctx(Ctx *c)
         c->aux = x;
     }
     c->aux->timing = c->timing;
+    c->aux->opt = c->opt;
     return c->aux;
 }
 
 static Ctx *sub_ctx(Ctx *c, size_t i)
 {
-    // a fourth pipeline (BMH_STREAMS=4) runs on stream D, the D2H / run-path side stream, which
+    // a fourth pipeline runs on stream D, the D2H / run-path side stream, which
     // device-resident batches past the run screen leave idle; later ones get streams of their own
     while (c->subs.size() <= i) new_sub(c, c->subs.size() == 3 ? c->s_d2h : nullptr)->aux_stream = c->s_d2h;
     Ctx *x = c->subs[i];
     x->timing = c->timing;
+    x->opt = c->opt;
     return x;
 }
 
@@ -281,14 +283,12 @@ static Ctx *sub_ctx(Ctx *c, size_t i)
 // queues and serialise: Calgary 7.9 ms).
 static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
 {
-    if (c->nstreams > 0) return c->nstreams;
-    const char *e = getenv("BMH_STREAMS");
-    const int v = e ? atoi(e) : 0;
+    const int v = (int)std::min<uint64_t>(c->opt.pipelines, 16);  // BMH_OPT_PIPELINES
     // (a third pipeline of few, large blocks leaves each with too little work per list round:
     // 128 MB of Zipf in 8 x 16 MiB blocks 21.35 -> 20.7 ms with 2). Batches past the run screen
     // (> 64 MiB) leave stream D idle: four pipelines, one per hardware queue (1 GiB random
     // 11.08-11.20 -> 10.96-10.98 ms; Zipf 100 MB at 1 MiB blocks 10.94 -> 10.65 ms).
-    if (v > 0) return std::min(v, 16);
+    if (v > 0) return v;
     if (nblocks >= 16 && total > (64ull << 20)) return 4;
     return total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
 }
@@ -384,18 +384,16 @@ static uint32_t pipelines_for(Ctx *c, uint64_t total, uint32_t nb, int max_pipes
     return S <= 1 ? 1u : S;
 }
 
-static uint64_t max_batch_bytes()
+static uint64_t max_batch_bytes(const Ctx *c)
 {
-    const char *e = getenv("BMH_MAX_BATCH");
-    uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+    const uint64_t v = c->opt.max_batch;  // BMH_OPT_MAX_BATCH
     return v ? v : (1ull << 30);
 }
 
-static uint64_t stream_batch_bytes()
+static uint64_t stream_batch_bytes(const Ctx *c)
 {
-    const char *e = getenv("BMH_STREAM_BATCH");
-    uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
-    return std::min<uint64_t>(v ? v : (256ull << 20), max_batch_bytes());
+    const uint64_t v = c->opt.stream_batch;  // BMH_OPT_STREAM_BATCH
+    return std::min<uint64_t>(v ? v : (256ull << 20), max_batch_bytes(c));
 }
 
 // memcpy on up to `nt` threads (pageable <-> pinned staging copies are CPU-bound)
@@ -501,7 +499,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
         std::vector<uint64_t> blocks, offs;
         uint64_t cap = 0;
     };
-    const uint64_t cap_batch = stream_batch_bytes();
+    const uint64_t cap_batch = stream_batch_bytes(c);
     // (a halving tail of batch sizes, to shorten the ramp-down after the last H2D, measured no
     // better: every new batch layout rebuilds the encode's tables on the host)
     std::vector<B> batches;
@@ -1158,8 +1156,8 @@ bmh_status bmh_decompress_dev(bmh_ctx *c, const uint8_t *in, uint64_t len, uint8
     *n_out = total;
     if (!out) return BMH_OK;
     if (total > cap) fail(BMH_ERANGE, "decompress: output capacity too small");
-    // batches of consecutive records: output < 1 GiB (BMH_MAX_BATCH), <= 65535 records
-    const uint64_t cap_batch = max_batch_bytes();
+    // batches of consecutive records: output < 1 GiB (BMH_OPT_MAX_BATCH), <= 65535 records
+    const uint64_t cap_batch = max_batch_bytes(c);
     uint64_t done = 0;
     for (size_t i = 0; i < ro.size();) {
         size_t j = i;
@@ -1216,6 +1214,28 @@ bmh_status bmh_container_record(const uint8_t *in, uint64_t len, uint64_t b, con
     if (o > len || l > len - o) fail(BMH_ECORRUPT, "container: record overruns input");
     if (rec) *rec = in + o;
     if (rec_len) *rec_len = l;
+    API_END
+}
+
+bmh_status bmh_ctx_set_option(bmh_ctx *c, uint32_t option, uint64_t value)
+{
+    API_BEGIN
+    use_device(c);
+    c->sync();
+    switch (option) {
+    case BMH_OPT_PIPELINES:
+        if (value > 16) fail(BMH_ERANGE, "set_option: at most 16 pipelines");
+        c->opt.pipelines = value;
+        break;
+    case BMH_OPT_STREAM_BATCH: c->opt.stream_batch = value; break;
+    case BMH_OPT_MAX_BATCH: c->opt.max_batch = value; break;
+    case BMH_OPT_MTF_CHUNK:
+        if (value > 4096 || (value && value < 64)) fail(BMH_ERANGE, "set_option: MTF chunk of 64..4096 symbols (0: adaptive)");
+        c->opt.mtf_chunk = value;
+        break;
+    case BMH_OPT_CHECK_LISTS: c->opt.check_lists = value != 0; break;
+    default: fail(BMH_EINVAL, "set_option: unknown option " + std::to_string(option));
+    }
     API_END
 }
 

@@ -42,38 +42,24 @@ constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 // while each lane walks 4096 steps (~1.2 ms whatever the batch size). Such batches take shorter
 // chunks, down to kMtfChunkMin, so they fill about one round; batches over kMtfAdaptiveMax
 // keep kMtfChunk.
-// BMH_MTF_CHUNK overrides it for experiments.
+// BMH_OPT_MTF_CHUNK (bmh_ctx_set_option) overrides it for experiments.
 constexpr uint32_t kMtfChunkMin = 256;
 // only batches up to this size adapt: a layout change rebuilds the MTF tables on the host, and
 // 128-256 MiB streamed batches measured slower with shorter chunks (31 -> 46 ms per GiB)
 constexpr uint64_t kMtfAdaptiveMax = 64ull << 20;
-static uint32_t mtf_chunk_len(int device, uint64_t total)
+static uint32_t mtf_chunk_len(const Ctx *c, uint64_t total)
 {
-    static const uint32_t env = [] {
-        const char *e = getenv("BMH_MTF_CHUNK");
-        return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-    }();
-    uint64_t x = env;
+    uint64_t x = c->opt.mtf_chunk;
     if (!x && total > kMtfAdaptiveMax) x = kMtfChunk;
     if (!x) {
-        // per-device CU count, cached (host threads of several contexts call this concurrently)
-        static std::atomic<int> cus[64] = {};
-        int cu = cus[device & 63].load(std::memory_order_relaxed);
-        if (!cu) {
-            if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cu = 256;
-            cus[device & 63].store(cu, std::memory_order_relaxed);
-        }
-        const uint64_t lanes = (uint64_t)std::max(cu, 1) * 6 * 64;
+        const uint64_t lanes = (uint64_t)std::max(c->cus, 1) * 6 * 64;
         x = std::max<uint64_t>(kMtfChunkMin, (total + lanes - 1) / lanes);
     }
     x = x < 64 ? 64 : (x > kMtfChunk ? kMtfChunk : x);
     return (uint32_t)((x + 63) & ~63ull);
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
-#ifndef BMH_MTF_AHEAD
-#define BMH_MTF_AHEAD 1
-#endif
-constexpr int kMtfAhead = BMH_MTF_AHEAD;  // symbols whose stamp reads run ahead of the update
+constexpr int kMtfAhead = 1;  // symbols whose stamp reads run ahead of the update
 
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
@@ -649,7 +635,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
 {
     const uint32_t nb = bt.nblocks;
     // chunk / composition tables: rebuilt and uploaded only when the batch layout changed
-    const uint32_t clen = mtf_chunk_len(c->device, bt.total);
+    const uint32_t clen = mtf_chunk_len(c, bt.total);
     const uint64_t sig = layout_sig(2, bt.offs, clen);
     uint32_t nch, nhh, ng, npk;
     if (c->ws_tag[WS_MTF_CHUNKS] == sig) {

@@ -126,7 +126,7 @@ bmh_status bmh_pack_dev(bmh_ctx *ctx, const uint8_t *d_mtf, const uint64_t *offs
 bmh_status bmh_encode_blocks_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64_t *offs, uint32_t nblocks,
                                  uint8_t *d_out, uint64_t out_cap, uint64_t *h_rec_offs);
 /* Pipelines (HIP streams, each driven by its own host thread) bmh_encode_blocks_dev runs a batch
- * of nblocks blocks totalling `total` bytes on (the library's rule; BMH_STREAMS overrides). */
+ * of nblocks blocks totalling `total` bytes on (the library's rule; BMH_OPT_PIPELINES overrides). */
 uint32_t bmh_encode_pipelines(bmh_ctx *ctx, uint64_t total, uint32_t nblocks);
 /* Capacity sufficient for one record of an n-byte block. */
 uint64_t bmh_record_bound(uint64_t n);
@@ -169,6 +169,19 @@ int bmh_is_container(const uint8_t *in, uint64_t len);
 bmh_status bmh_container_info(const uint8_t *in, uint64_t len, uint64_t *nblocks, uint64_t *total_n);
 /* Pointer/length of record b inside a container. */
 bmh_status bmh_container_record(const uint8_t *in, uint64_t len, uint64_t b, const uint8_t **rec, uint64_t *rec_len);
+
+/* ---- tuning options ---------------------------------------------------------------- */
+/* Per-context overrides of the library's own rules (not part of the reference interface; the
+ * library reads no environment variables). Value 0 restores the default. Results never depend
+ * on them: every setting produces the same records. */
+enum {
+    BMH_OPT_PIPELINES = 1,    /* pipelines (streams) per device batch, 1..16 (default: the size rule) */
+    BMH_OPT_STREAM_BATCH = 2, /* bmh_compress_host batch bytes (default 256 MiB) */
+    BMH_OPT_MAX_BATCH = 3,    /* largest device batch bytes of the host-buffer paths (default 1 GiB) */
+    BMH_OPT_MTF_CHUNK = 4,    /* MTF chunk symbols, 64..4096 (default: adaptive) */
+    BMH_OPT_CHECK_LISTS = 5   /* 1: check every BWT list round and print its census (diagnostic, slow) */
+};
+bmh_status bmh_ctx_set_option(bmh_ctx *ctx, uint32_t option, uint64_t value);
 
 /* ---- measurement ------------------------------------------------------------------- */
 /* When enabled, every kernel launch of the context is bracketed by HIP events on the

@@ -34,7 +34,7 @@ def test_world2_bench_on_gpu(scaling):
     env = dict(os.environ)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(REPO, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling]
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--scaling", scaling, "--cpu-procs", "2"]
     if scaling == "weak":  # 64 blocks per rank, every leg of the default line
         cmd += ["--bytes-per-gpu", str(256 << 20), "--decode-steps", "1", "--pcie-steps", "1", "--calgary-steps", "1"]
     else:  # config 4 as written (1 GiB dealt over the ranks) + the 1 GiB-per-GPU leg, here 256 MiB
@@ -47,7 +47,9 @@ def test_world2_bench_on_gpu(scaling):
     assert line["value"] > 0 and line["ms_per_step"] > 0
     nblk = 128 if scaling == "weak" else 256  # blocks over both ranks
     assert line["parity"] == f"{nblk}/{nblk} records byte-identical to the reference manifest", line["parity"]
-    assert line["cpu_baseline"] is None  # N > 1: the CPU baseline is an N = 1 leg
+    # rank 0 times the reference CPU path at any world size (here on 2 processes to stay short)
+    cb = line["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] == "reference", cb
     # the pipelines the library really runs for the rank's batch (capi.cpp stream_count)
     assert line["config"]["streams_per_gpu"] == 4
     if scaling == "strong":

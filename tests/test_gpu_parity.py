@@ -427,19 +427,25 @@ def test_container_roundtrip(ctx):
     assert recs[0] == one
 
 
-def test_streamed_host_compress_many_batches(ctx, monkeypatch):
+def test_streamed_host_compress_many_batches(ctx):
     """bmh_compress_host's pipeline (staging slots, side-stream H2D/D2H) over many small
     batches, one and two contexts: the container equals the per-block device records."""
     data = synth.zipf_text(9_000_017).tobytes()
     bs = 1 << 20
     blocks = [data[i:i + bs] for i in range(0, len(data), bs)]
     want = ctx.encode_blocks(blocks)
-    for batch in (bs, 3 * bs + 5, 1 << 30):  # 9, 3 and 1 batches
-        monkeypatch.setenv("BMH_STREAM_BATCH", str(batch))
-        out = ctx.compress_bytes(data, block_size=bs)
-        assert bmh.container_records(out) == want, batch
-        multi = bmh.compress_bytes_multi([ctx, bmh.Context(0)], data, bs)
-        assert multi == out, batch
+    other = bmh.Context(0)
+    try:
+        for batch in (bs, 3 * bs + 5, 1 << 30):  # 9, 3 and 1 batches
+            for c in (ctx, other):
+                c.set_option("stream_batch", batch)
+            out = ctx.compress_bytes(data, block_size=bs)
+            assert bmh.container_records(out) == want, batch
+            multi = bmh.compress_bytes_multi([ctx, other], data, bs)
+            assert multi == out, batch
+    finally:
+        ctx.set_option("stream_batch", 0)
+        other.close()
     assert bmh.decompress_bytes(out) == data
 
 
@@ -645,11 +651,11 @@ def test_device_errors_are_status_codes(ctx):
     assert ctx.decompress_bytes(ctx.encode_blocks([a.tobytes()])[0]) == a.tobytes()
 
 
-def test_compress_host_pinned_buffers(ctx, monkeypatch):
+def test_compress_host_pinned_buffers(ctx):
     """bmh_compress_host with page-locked input and output (bmh_host_alloc: DMA-only path,
     records D2H'd straight to their place) writes the same bytes as with pageable buffers;
     several stream batches, a single block, and a too-small page-locked output (ERANGE)."""
-    monkeypatch.setenv("BMH_STREAM_BATCH", str(3 << 20))
+    ctx.set_option("stream_batch", 3 << 20)
     data = np.frombuffer(synth.zipf_text(10_000_019).tobytes(), np.uint8)
     hin = ctx.alloc_host(data.size)
     hin.a[:] = data
@@ -674,6 +680,7 @@ def test_compress_host_pinned_buffers(ctx, monkeypatch):
         assert ctx.decompress_bytes(ctx.compress_bytes(data[:5000], 0)) == data[:5000].tobytes()
     finally:
         hin.free()
+        ctx.set_option("stream_batch", 0)
 
 
 def test_compress_host_multi_matches_single_context(ctx):
@@ -882,3 +889,34 @@ def test_compacted_alphabet_global_pass(ctx, oracle):
     recs = ctx.encode_blocks(allb)
     for i in rec_check:
         assert recs[i] == oracle.encode(blocks[i]), (i, len(blocks[i]))
+
+
+def test_tuning_options_never_change_records(ctx):
+    """Every non-default bmh_ctx_set_option value (include/bmh.h BMH_OPT_*) once: pipelines 1..4
+    and 5, MTF chunks 64 / 1024 / 4096, the list-round checker, and small stream / max batches on
+    the host-buffer path, against the default encode of a mixed batch (random, Zipf text, a
+    run-heavy block, tiny blocks). Unknown options and out-of-range values are status codes."""
+    rng = np.random.default_rng(5)
+    blocks = [rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes() for _ in range(6)]
+    z = synth.zipf_text(6 << 20).tobytes()
+    blocks += [z[i:i + (1 << 20)] for i in range(0, len(z), 1 << 20)]
+    blocks += [bytes(200000) + b"\x01" * 100000, b"banana", b"a" * 40, rng.integers(0, 4, 70000, np.uint8).tobytes()]
+    want = ctx.encode_blocks(blocks)
+    try:
+        for name, vals in (("pipelines", (1, 2, 3, 4, 5)), ("mtf_chunk", (64, 1024, 4096)), ("check_lists", (1,))):
+            for v in vals:
+                ctx.set_option(name, v)
+                assert ctx.encode_blocks(blocks) == want, (name, v)
+            ctx.set_option(name, 0)
+        data = b"".join(blocks[:12])
+        ref = ctx.compress_bytes(data, block_size=1 << 20)
+        for name, v in (("stream_batch", 3 << 20), ("max_batch", 2 << 20)):
+            ctx.set_option(name, v)
+            assert ctx.compress_bytes(data, block_size=1 << 20) == ref, name
+            assert ctx.decompress_bytes(ref) == data, name
+            ctx.set_option(name, 0)
+    finally:
+        for name in bmh.Context.OPTIONS:
+            ctx.set_option(name, 0)
+    for opt, v, st in ((99, 1, 1), (1, 17, 4), (4, 5000, 4), (4, 10, 4)):
+        assert bmh.lib().bmh_ctx_set_option(ctx.h, opt, v) == st, (opt, v)

@@ -6,6 +6,5 @@ export TMPDIR=/tmp
 o=gpurun_out/cal2; mkdir -p $o
 files="bib book1 book2 geo news obj1 obj2 paper1 paper2 pic progc progl progp trans"
 timeout -k 10 120 rocprofv3 --kernel-trace -d $o/t -o run --output-format csv -- python3 tools/cal_trace_run.py $files > $o/log 2>&1
-export BMH_STREAMS=1
-timeout -k 10 120 rocprofv3 --kernel-trace -d $o/t1 -o run --output-format csv -- python3 tools/cal_trace_run.py $files > $o/log1 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace -d $o/t1 -o run --output-format csv -- python3 tools/cal_trace_run.py --opts pipelines=1 $files > $o/log1 2>&1
 echo ok

@@ -3,7 +3,7 @@ mkdir -p gpurun_out/mtfsw
 for c in 0 2048 1024; do
   for cfg in "100 1" "128 16"; do
     if [ $c = 0 ]; then timeout -k 10 120 python3 tools/text_bench.py $cfg > gpurun_out/mtfsw/t_${c}_${cfg// /_}.json
-    else BMH_MTF_CHUNK=$c timeout -k 10 120 python3 tools/text_bench.py $cfg > gpurun_out/mtfsw/t_${c}_${cfg// /_}.json; fi
+    else timeout -k 10 120 python3 tools/text_bench.py $cfg mtf_chunk=$c > gpurun_out/mtfsw/t_${c}_${cfg// /_}.json; fi
   done
 done
 python3 - <<'P'

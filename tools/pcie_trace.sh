@@ -8,10 +8,8 @@ o=gpurun_out/pcie; mkdir -p $o
 args="--steps 2 --warmup 1 --no-cpu-baseline --decode-steps 0 --calgary-steps 0 --pcie-steps 2"
 timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d $o/b256 -o run --output-format csv -- python3 bench.py $args > $o/b256.json 2> $o/b256.err
 python3 tools/pcie_timeline.py $o/b256 40 > $o/timeline_256m.txt
-export BMH_STREAM_BATCH=$((64 << 20))
-timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d $o/b64 -o run --output-format csv -- python3 bench.py $args > $o/b64.json 2> $o/b64.err
+timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace -d $o/b64 -o run --output-format csv -- python3 bench.py $args --opt stream_batch=$((64 << 20)) > $o/b64.json 2> $o/b64.err
 python3 tools/pcie_timeline.py $o/b64 50 > $o/timeline_64m.txt
-unset BMH_STREAM_BATCH
 timeout -k 10 200 python3 bench.py $args > $o/plain256.json 2> $o/plain256.err
-BMH_STREAM_BATCH=$((64 << 20)) timeout -k 10 200 python3 bench.py $args > $o/plain64.json 2> $o/plain64.err
+timeout -k 10 200 python3 bench.py $args --opt stream_batch=$((64 << 20)) > $o/plain64.json 2> $o/plain64.err
 echo pcie trace done

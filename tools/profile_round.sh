@@ -9,8 +9,8 @@ o=gpurun_out/prof
 mkdir -p $o
 timeout -k 10 400 python3 bench.py > $o/bench.json 2> $o/bench.err
 # one stream, like bench.py's per-kernel pass, so the per-kernel durations agree with its roofline
-BMH_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/stats -o run --output-format csv -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 > $o/stats_bench.json 2> $o/stats.err
-BMH_STREAMS=1 PMC_GROUPS="FETCH_SIZE;WRITE_SIZE" timeout -k 10 600 bash tools/pmc_run.sh $o/pmc --steps 2 --warmup 1 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $o/stats -o run --output-format csv -- \
+    python3 bench.py --pipelines 1 --steps 5 --warmup 1 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 > $o/stats_bench.json 2> $o/stats.err
+PMC_GROUPS="FETCH_SIZE;WRITE_SIZE" timeout -k 10 600 bash tools/pmc_run.sh $o/pmc --steps 2 --warmup 1 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 --pipelines 1
 python3 tools/pmc_traffic.py $o/pmc $((1 << 30)) $o/pmc_traffic.json
 echo profile done

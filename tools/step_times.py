@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-step wall times of the bench workload (1 GiB random, 4 MiB blocks) over many steps,
-to expose warm-up / power-state effects. usage: python tools/step_times.py [steps]"""
+to expose warm-up / power-state effects. usage: python tools/step_times.py [steps] [options]"""
 import os
 import sys
 import time
@@ -12,6 +12,7 @@ import bmh  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 ctx = bmh.Context(0)
+ctx.set_options(sys.argv[2] if len(sys.argv) > 2 else "")
 bs, nblk = 4 << 20, 256
 offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
 d_in = ctx.alloc(bs * nblk)

@@ -5,8 +5,8 @@ tag=$1; v=$2
 run() {  # $1 = label, env BMH_LIB set by the caller
   timeout -k 10 200 python3 tools/text_bench.py 100 1 > gpurun_out/${tag}_$1_text100.json 2> /dev/null || return 1
   timeout -k 10 200 python3 tools/text_bench.py 128 16 > gpurun_out/${tag}_$1_text128.json 2> /dev/null || return 1
-  BMH_DBG_LISTS=1 timeout -k 10 200 python3 tools/list_census.py 100 1 > /dev/null 2> gpurun_out/${tag}_$1_census100.txt || return 1
-  BMH_DBG_LISTS=1 timeout -k 10 200 python3 tools/list_census.py 128 16 > /dev/null 2> gpurun_out/${tag}_$1_census128.txt || return 1
+  timeout -k 10 200 python3 tools/list_census.py 100 1 > /dev/null 2> gpurun_out/${tag}_$1_census100.txt || return 1
+  timeout -k 10 200 python3 tools/list_census.py 128 16 > /dev/null 2> gpurun_out/${tag}_$1_census128.txt || return 1
 }
 run lib || exit 1
 BMH_LIB=variants/$v/libbmh.so run $v || exit 1

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Encode throughput on Zipf text — configs 3 (100 MB, 1 MiB blocks) and 5
-(16 MiB blocks) — with the per-kernel breakdown. usage: python tools/text_bench.py [MB] [block_MiB]"""
+(16 MiB blocks) — with the per-kernel breakdown. usage: python tools/text_bench.py [MB] [block_MiB] [options]
+(options: "name=value,..." for bmh_ctx_set_option, e.g. mtf_chunk=2048)"""
 import hashlib
 import json
 import os
@@ -18,7 +19,9 @@ mb = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 bs = (int(sys.argv[2]) if len(sys.argv) > 2 else 1) << 20
 n = mb * 1000 * 1000
 z = synth.zipf_text(n)
+opts = sys.argv[3] if len(sys.argv) > 3 else ""
 ctx = bmh.Context(0)
+ctx.set_options(opts)
 nb = (n + bs - 1) // bs
 offs = np.minimum(np.arange(nb + 1, dtype=np.uint64) * np.uint64(bs), np.uint64(n))
 d_in = ctx.alloc(n)
@@ -31,7 +34,7 @@ steps = 3
 for _ in range(steps):
     ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
 dt = (time.perf_counter() - t0) / steps
-os.environ["BMH_STREAMS"] = "1"
+ctx.set_option("pipelines", 1)  # per-kernel times of one stream
 ctx.reset_stats()
 ctx.set_timing(True)
 ctx.encode_blocks_dev(d_in, offs, d_out, cap)

@@ -4,8 +4,8 @@
 tag=${1:-t}
 timeout -k 10 200 python3 tools/text_bench.py 100 1 > gpurun_out/${tag}_text100.json 2> gpurun_out/${tag}_text100.err || exit 1
 timeout -k 10 200 python3 tools/text_bench.py 128 16 > gpurun_out/${tag}_text128.json 2> gpurun_out/${tag}_text128.err || exit 1
-BMH_DBG_LISTS=1 timeout -k 10 200 python3 tools/list_census.py 100 1 > /dev/null 2> gpurun_out/${tag}_census100.txt || exit 1
-BMH_DBG_LISTS=1 timeout -k 10 200 python3 tools/list_census.py 128 16 > /dev/null 2> gpurun_out/${tag}_census128.txt || exit 1
+timeout -k 10 200 python3 tools/list_census.py 100 1 > /dev/null 2> gpurun_out/${tag}_census100.txt || exit 1
+timeout -k 10 200 python3 tools/list_census.py 128 16 > /dev/null 2> gpurun_out/${tag}_census128.txt || exit 1
 python3 - "$tag" <<'P'
 import json, sys
 t = sys.argv[1]
