@@ -77,6 +77,7 @@ _SIGS = {
     "bmh_encode_blocks_dev": (C.c_int, [P, P, PU64, U32, P, U64, PU64]),
     "bmh_record_bound": (U64, [U64]),
     "bmh_encode_pipelines": (U32, [P, U64, U32]),
+    "bmh_ctx_last_pipelines": (U32, [P]),
     "bmh_compress_host": (C.c_int, [P, P, U64, U64, P, U64, PU64]),
     "bmh_compress_host_multi": (C.c_int, [C.POINTER(P), U32, P, U64, U64, P, U64, PU64]),
     "bmh_compress_bound": (U64, [U64, U64]),
@@ -239,8 +240,13 @@ class Context:
         return n.value
 
     def pipelines(self, total: int, nblocks: int) -> int:
-        """Pipelines (streams) the library runs a device batch of this shape on."""
+        """Pipelines (streams) the library's rule gives a device batch of this shape (before the
+        data probe: see last_pipelines)."""
         return int(lib().bmh_encode_pipelines(self.h, total, nblocks))
+
+    def last_pipelines(self) -> int:
+        """Pipelines the last encode_blocks_dev call ran on."""
+        return int(lib().bmh_ctx_last_pipelines(self.h))
 
     # ---- tuning options (include/bmh.h BMH_OPT_*; 0 restores the library's rule)
     OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5}

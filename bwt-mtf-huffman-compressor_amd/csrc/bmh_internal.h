@@ -100,6 +100,10 @@ struct Ctx {
     struct Options {
         uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0;
     } opt;
+    uint32_t last_pipelines = 0;
+    uint64_t zipf_resume_tok0 = 0, zipf_resume_base = 0;  // synth_zipf: start of its last round  // pipelines of the last device batch encode (encode_blocks)
+    uint64_t mtf_clen_sig = 0;  // MTF chunk length of the last batch layout (mtf.hip)
+    uint32_t mtf_clen = 0;
     // size of the batch a sub-pipeline's sub-batch was cut from (0: its own batch): the run
     // screen is decided on it, so a batch past the screen never sends its sub-batches' run-heavy
     // blocks to the side stream D, which a fourth pipeline holds (bwt_runs.hip)
@@ -204,6 +208,7 @@ constexpr uint32_t kStatusEmpty = 1, kStatusCodeLen = 2, kStatusPrimary = 4, kSt
 // return host outputs (h_primary / h_freq32 non-null).
 void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);  // bwt_runs.hip
 Ctx *aux_ctx(Ctx *c);  // capi.cpp
+bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt);  // digram census (bwt_runs.hip)
 // the rotation sorter alone (bwt.hip); bwt_batch routes run-heavy blocks of small batches around it
 void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,
@@ -244,7 +249,9 @@ struct BandRanks {
     std::vector<uint16_t> rank;  // node id -> ascending-address rank among the 2L - 1 nodes
 };
 std::shared_ptr<const BandRanks> band_ranks(uint64_t n);  // LRU-bounded cache (heap_order.cpp)
-void band_ranks_prefetch(const std::vector<uint64_t> &sizes);  // computes the missing ones in parallel
+// the tables of a batch's sizes (< kBandCeil), the missing ones computed in parallel; the
+// returned pointers outlive any eviction from the cache
+std::map<uint64_t, std::shared_ptr<const BandRanks>> band_ranks_batch(const std::vector<uint64_t> &sizes);
 size_t band_cache_entries();  // sizes currently cached
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank);  // exact ranks (model or heap history)
 uint64_t payload_bytes(const bmh_code_table *t, const uint64_t freq[256]);

@@ -44,9 +44,43 @@ namespace {
 
 constexpr uint64_t kRunScreenMax = 64ull << 20;  // batches screened for run-heavy blocks
 constexpr uint32_t kRunMinBlock = 1u << 16;      // shorter blocks stay on the rotation sorter
-constexpr uint32_t kRunMaxBlock = 1u << 24;      // run lengths and ranks fit 24 bits of the key
+constexpr uint32_t kRunMaxBlock = 1u << 24;      // run lengths fit 24 bits of the key
+// The position key's low 24 bits hold a run's rank among ALL runs of a run batch (blocks are
+// sorted together, run_blocks_batch), so a batch's runs M must stay below 2^24: run_blocks groups
+// close before that. One screened batch can never reach it (runs <= n / kRunShare per block).
+constexpr uint32_t kRunRankLimit = 1u << 24;
 constexpr uint32_t kRunShare = 4;                // run-heavy: runs <= n / kRunShare
 constexpr uint32_t kMask24 = (1u << 24) - 1;
+static_assert(kRunScreenMax / kRunShare <= kRunRankLimit, "a screened batch's runs fit the 24-bit rank field");
+
+// Digram census (dense_batch): distinct byte pairs among the first kProbeSample positions of each
+// block, one workgroup a block, a 65 536-bit LDS bitmap. Uniform-random bytes give ~14.5 K
+// distinct pairs in 16 K positions, text a few hundred to a few thousand.
+constexpr uint32_t kProbeSample = 16384;
+__global__ __launch_bounds__(256) void k_probe_digrams(const uint8_t *__restrict__ in, const uint64_t *__restrict__ boffs,
+                                                       uint32_t *__restrict__ out)
+{
+    __shared__ uint32_t bm[2048];
+    __shared__ uint32_t s_tot;
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    const uint64_t o = boffs[b];
+    const uint32_t m = (uint32_t)min<uint64_t>(boffs[b + 1] - o, kProbeSample);
+    for (uint32_t i = t; i < 2048; i += 256) bm[i] = 0;
+    if (t == 0) s_tot = 0;
+    __syncthreads();
+    const uint8_t *x = in + o;
+    for (uint32_t i = t; i + 1 < m; i += 256) {
+        const uint32_t d = ((uint32_t)x[i] << 8) | x[i + 1];
+        atomicOr(&bm[d >> 5], 1u << (d & 31u));
+    }
+    __syncthreads();
+    uint32_t k = 0;
+    for (uint32_t i = t; i < 2048; i += 256) k += __builtin_popcount(bm[i]);
+    k = wave_sum_dpp(k);
+    if ((t & 63u) == 0) atomicAdd(&s_tot, k);
+    __syncthreads();
+    if (t == 0) out[b] = s_tot;
+}
 
 // Run heads per block: grid (tiles of 4096 positions, blocks); thread t takes 16 positions.
 __global__ __launch_bounds__(256) void k_run_count(const uint8_t *__restrict__ in, const uint64_t *__restrict__ boffs,
@@ -546,6 +580,9 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
     const uint32_t B = (uint32_t)offs.size();
     if (B == 0) return;
     if (B > kRunBatchBlocks) fail(BMH_EINVAL, "bwt: too many run blocks in one batch");
+    uint64_t Mtot = 0;
+    for (uint32_t m : ms) Mtot += m;
+    if (Mtot >= kRunRankLimit) fail(BMH_EINVAL, "bwt: too many runs in one run batch (24-bit ranks)");
     std::vector<RBlk> tab(B);
     uint64_t N = 0;
     uint32_t M = 0, NT = 0, maxn = 0, maxm = 0;
@@ -583,6 +620,31 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
     BMH_LAUNCH(c, "bwt_run_out", k_brun_out, dim3(cdiv(maxn, 256), B), 256, 0, in, w.tab, w.pval2, L, prim);
 }
 }  // namespace
+
+// Whether a batch is dense (uniform-like bytes: the BWT's two data passes resolve it with one
+// short list round, no host-synchronised rounds), by the digram census of each block's first
+// 16 K positions: at least half of the sampled pairs distinct, for blocks holding >= 90 % of the
+// bytes. One launch and one host wait (~20-30 us). encode_blocks runs such batches on one
+// pipeline: on random data the pipelines only contend (128 MiB: 1.77 ms on one, 1.99 on four).
+bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt)
+{
+    const uint32_t nb = bt.nblocks;
+    uint8_t *d_misc = (uint8_t *)c->get(WS_RUN_MISC, (size_t)(nb + 1) * 8 + (size_t)nb * 8 + 1024);
+    uint64_t *d_boffs = (uint64_t *)d_misc;
+    uint32_t *d_count = (uint32_t *)(d_misc + (size_t)(nb + 1) * 8);
+    std::vector<uint32_t> cnt(nb);
+    c->h2d(d_boffs, bt.offs.data(), (size_t)(nb + 1) * 8);
+    BMH_LAUNCH(c, "probe_digrams", k_probe_digrams, nb, 256, 0, d_in, d_boffs, d_count);
+    c->d2h(cnt.data(), d_count, (size_t)nb * 4);
+    c->sync();
+    uint64_t dense = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t n = bt.offs[b + 1] - bt.offs[b];
+        const uint64_t m = std::min<uint64_t>(n, kProbeSample);
+        if (m >= 4096 && 2ull * cnt[b] >= m) dense += n;
+    }
+    return dense * 10 >= bt.total * 9;
+}
 
 // Batch BWT: small batches are screened for run-heavy blocks, which take the run path above;
 // every other block goes through the rotation sorter (bwt_batch_core), gathered into one
@@ -631,16 +693,20 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
         uint32_t *p = (uint32_t *)x->get(WS_RUN_PRIM, rb.size() * 4 + 64);
         uint32_t h_cnt = 0;
         // all run blocks sorted together (one host wait a doubling round for all of them), in
-        // groups of at most kRunBatchBlocks
-        for (size_t g = 0; g < rb.size(); g += kRunBatchBlocks) {
+        // groups of at most kRunBatchBlocks blocks and fewer than kRunRankLimit runs
+        for (size_t g = 0; g < rb.size();) {
             std::vector<uint64_t> offs;
             std::vector<uint32_t> ns, ms;
-            for (size_t i = g; i < std::min(rb.size(), g + kRunBatchBlocks); ++i) {
+            uint64_t m = 0;
+            size_t i = g;
+            for (; i < rb.size() && i - g < kRunBatchBlocks && (i == g || m + runs[rb[i]] < kRunRankLimit); ++i) {
                 offs.push_back(bt.offs[rb[i]]);
                 ns.push_back((uint32_t)(bt.offs[rb[i] + 1] - bt.offs[rb[i]]));
                 ms.push_back(runs[rb[i]]);
+                m += runs[rb[i]];
             }
             run_blocks_batch(x, d_in, offs, ns, ms, d_L, p + g, &h_cnt);
+            g = i;
         }
         rp = p;
     };

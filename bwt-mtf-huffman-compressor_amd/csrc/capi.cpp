@@ -294,6 +294,7 @@ static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
 }
 
 static uint32_t pipelines_for(Ctx *c, uint64_t total, uint32_t nb, int max_pipes);
+constexpr uint64_t kDenseProbeMin = 32ull << 20, kDenseProbeMax = 256ull << 20;
 
 // The batch is cut into S runs of whole blocks (balanced by bytes), each encoded on its own
 // stream by its own host thread, so that one run's bandwidth-bound kernels overlap another's
@@ -303,7 +304,15 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
                    uint64_t *rec_offs, int max_pipes)
 {
     const uint32_t nb = bt.nblocks;
-    const int S = (int)pipelines_for(c, bt.total, nb, max_pipes);
+    int S = (int)pipelines_for(c, bt.total, nb, max_pipes);
+    // dense batches of 32-256 MiB run on one pipeline (dense_batch): on random data four
+    // pipelines only contend (128 / 256 MiB of 4 MiB blocks: 1.99 / 3.49 ms against 1.77 / 3.14
+    // on one; 1 GiB: equal), while text keeps them for its host-synchronised list rounds
+    // (Zipf 128 MB at 4 MiB blocks: 14.1 ms on four, 16.8 on one)
+    if (S > 1 && !c->opt.pipelines && bt.total >= kDenseProbeMin && bt.total <= kDenseProbeMax &&
+        dense_batch(c, d_in, bt))
+        S = 1;
+    c->last_pipelines = (uint32_t)std::max(S, 1);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
         return;
@@ -972,8 +981,10 @@ int bmh_node_ranks(uint64_t n, uint32_t L, uint16_t *rank)
 uint32_t bmh_encode_pipelines(bmh_ctx *c, uint64_t total, uint32_t nblocks)
 {
     if (!c || nblocks == 0) return 0;
-    return pipelines_for(c, total, nblocks, 16);  // as bmh_encode_blocks_dev
+    return pipelines_for(c, total, nblocks, 16);  // as bmh_encode_blocks_dev, before its data probe
 }
+
+uint32_t bmh_ctx_last_pipelines(bmh_ctx *c) { return c ? c->last_pipelines : 0u; }
 
 uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
 {

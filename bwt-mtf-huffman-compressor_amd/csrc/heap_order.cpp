@@ -564,37 +564,40 @@ std::shared_ptr<const BandRanks> band_ranks(uint64_t n)
     return it->second.r;
 }
 
-void band_ranks_prefetch(const std::vector<uint64_t> &sizes)
+std::map<uint64_t, std::shared_ptr<const BandRanks>> band_ranks_batch(const std::vector<uint64_t> &sizes)
 {
+    // every distinct size's table, the missing ones computed in parallel; the returned
+    // shared_ptrs keep the batch's tables alive even if the LRU cache evicts them meanwhile
     std::vector<uint64_t> todo;
-    {
-        std::lock_guard<std::mutex> lk(g_band_mu);
-        for (uint64_t n : sizes)
-            if (n && n < kBandCeil && !g_band.count(n)) todo.push_back(n);
-    }
+    for (uint64_t n : sizes)
+        if (n && n < kBandCeil) todo.push_back(n);
     std::sort(todo.begin(), todo.end());
     todo.erase(std::unique(todo.begin(), todo.end()), todo.end());
-    if (todo.size() < 2) {
-        for (uint64_t n : todo) band_ranks(n);
-        return;
-    }
+    std::vector<std::shared_ptr<const BandRanks>> got(todo.size());
     const unsigned nt = std::min<unsigned>((unsigned)todo.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
-    std::atomic<size_t> next{0};
-    std::mutex emu;
-    std::exception_ptr err;  // the first failure of a worker, rethrown on this thread
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < nt; ++t)
-        th.emplace_back([&] {
-            try {
-                for (size_t i; (i = next.fetch_add(1)) < todo.size();) band_ranks(todo[i]);
-            } catch (...) {
-                std::lock_guard<std::mutex> lk(emu);
-                if (!err) err = std::current_exception();
-                next.store(todo.size());
-            }
-        });
-    for (auto &x : th) x.join();
-    if (err) std::rethrow_exception(err);
+    if (nt <= 1) {
+        for (size_t i = 0; i < todo.size(); ++i) got[i] = band_ranks(todo[i]);
+    } else {
+        std::atomic<size_t> next{0};
+        std::mutex emu;
+        std::exception_ptr err;  // the first failure of a worker, rethrown on this thread
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([&] {
+                try {
+                    for (size_t i; (i = next.fetch_add(1)) < todo.size();) got[i] = band_ranks(todo[i]);
+                } catch (...) {
+                    std::lock_guard<std::mutex> lk(emu);
+                    if (!err) err = std::current_exception();
+                    next.store(todo.size());
+                }
+            });
+        for (auto &x : th) x.join();
+        if (err) std::rethrow_exception(err);
+    }
+    std::map<uint64_t, std::shared_ptr<const BandRanks>> out;
+    for (size_t i = 0; i < todo.size(); ++i) out.emplace(todo[i], std::move(got[i]));
+    return out;
 }
 
 void node_ranks(uint64_t n, uint32_t L, uint16_t *rank)

@@ -484,16 +484,15 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         std::vector<uint32_t> rbase(nb, kModelOrder), idx;
         std::vector<uint16_t> ranks;
         std::map<uint64_t, uint32_t> seen;
-        {
-            std::vector<uint64_t> sizes;
-            for (uint32_t b = 0; b < nb; ++b)
-                if (bt.offs[b + 1] - bt.offs[b] < kBandCeil) sizes.push_back(bt.offs[b + 1] - bt.offs[b]);
-            band_ranks_prefetch(sizes);
-        }
+        std::vector<uint64_t> sizes;
+        for (uint32_t b = 0; b < nb; ++b)
+            if (bt.offs[b + 1] - bt.offs[b] < kBandCeil) sizes.push_back(bt.offs[b + 1] - bt.offs[b]);
+        const auto tabs = band_ranks_batch(sizes);  // held until the upload below
         for (uint32_t b = 0; b < nb; ++b) {
             const uint64_t n = bt.offs[b + 1] - bt.offs[b];
-            const auto br = band_ranks(n);
-            if (!br) continue;
+            const auto it_t = tabs.find(n);
+            if (it_t == tabs.end() || !it_t->second) continue;
+            const auto &br = it_t->second;
             auto it = seen.find(n);
             if (it == seen.end()) {
                 const uint32_t at = (uint32_t)idx.size();

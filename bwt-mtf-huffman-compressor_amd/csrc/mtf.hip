@@ -37,26 +37,45 @@ namespace {
 constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 
 // Chunk length used by the host tables (<= kMtfChunk, a multiple of 64; the kernels take any
-// such length). One lane walks a chunk, about 6 one-wave workgroups fit a CU (LDS), and a step
-// takes ~0.3 us: a batch with fewer chunks than one resident round of lanes leaves the GPU idle
-// while each lane walks 4096 steps (~1.2 ms whatever the batch size). Such batches take shorter
-// chunks, down to kMtfChunkMin, so they fill about one round; batches over kMtfAdaptiveMax
-// keep kMtfChunk.
+// such length). One lane walks a chunk and every lane takes the same time per symbol, so the
+// encode runs in rounds of resident lanes (kMtfWgPerCu one-wave workgroups per CU, LDS-bound)
+// and costs rounds x chunk length steps. The length is chosen so the batch's chunks fill whole
+// rounds: R = the rounds kMtfChunk-symbol chunks need, then the shortest length (>=
+// kMtfChunkMin) whose chunks fit in R rounds. 4096-symbol chunks put 1 GiB of 4 MiB blocks in
+// 2.67 rounds, i.e. 3 rounds of 4096 steps; 3648-symbol chunks fill 3 rounds of 3648. A 256 MiB
+// batch in four pipelines: each 256 MiB sub-batch gets a quarter of the slots (3 rounds of 3648).
+// 128 MiB (the strong-scaling N = 8 share) fits one round of 1408 instead of a third of a round
+// of 4096.
 // BMH_OPT_MTF_CHUNK (bmh_ctx_set_option) overrides it for experiments.
 constexpr uint32_t kMtfChunkMin = 256;
-// only batches up to this size adapt: a layout change rebuilds the MTF tables on the host, and
-// 128-256 MiB streamed batches measured slower with shorter chunks (31 -> 46 ms per GiB)
-constexpr uint64_t kMtfAdaptiveMax = 64ull << 20;
-static uint32_t mtf_chunk_len(const Ctx *c, uint64_t total)
+constexpr uint32_t kMtfWgPerCu = 6;  // k_mtf_encode: 23.5 KB of LDS per one-wave workgroup
+static uint64_t mtf_chunk_count(const Batch &bt, uint64_t x)
 {
-    uint64_t x = c->opt.mtf_chunk;
-    if (!x && total > kMtfAdaptiveMax) x = kMtfChunk;
-    if (!x) {
-        const uint64_t lanes = (uint64_t)std::max(c->cus, 1) * 6 * 64;
-        x = std::max<uint64_t>(kMtfChunkMin, (total + lanes - 1) / lanes);
+    uint64_t k = 0;
+    for (uint32_t b = 0; b < bt.nblocks; ++b) {
+        const uint64_t o = bt.offs[b], n = bt.offs[b + 1] - o;
+        const uint64_t pre = std::min<uint64_t>(n, (64 - (o & 63u)) & 63u);  // unaligned first chunk
+        k += (pre != 0) + (n - pre + x - 1) / x;
     }
-    x = x < 64 ? 64 : (x > kMtfChunk ? kMtfChunk : x);
-    return (uint32_t)((x + 63) & ~63ull);
+    return k;
+}
+static uint32_t mtf_chunk_len(Ctx *c, const Batch &bt)
+{
+    if (c->opt.mtf_chunk) return (uint32_t)c->opt.mtf_chunk;
+    const uint64_t sig = layout_sig(4, bt.offs, 0) ^ (c->screen_total * 0x9e3779b97f4a7c15ull);
+    if (c->mtf_clen_sig == sig) return c->mtf_clen;
+    // a pipeline's sub-batch (capi.cpp encode_blocks) gets its byte share of the lane slots: the
+    // pipelines' encodes share the device (each filling it alone made a 128 MiB batch's four
+    // pipelines walk 384-symbol chunks, 11 K chunks a block through the composition)
+    const uint64_t whole = c->screen_total > bt.total ? c->screen_total : bt.total;
+    const uint64_t slots = std::max<uint64_t>(64, (uint64_t)std::max(c->cus, 1) * kMtfWgPerCu * 64 * bt.total / whole);
+    const uint64_t R = std::max<uint64_t>(1, (mtf_chunk_count(bt, kMtfChunk) + slots - 1) / slots);
+    uint64_t x = std::max<uint64_t>(kMtfChunkMin, ((bt.total + R * slots - 1) / (R * slots) + 63) & ~63ull);
+    while (x < kMtfChunk && mtf_chunk_count(bt, x) > R * slots) x += 64;
+    x = std::min<uint64_t>(x, kMtfChunk);
+    c->mtf_clen_sig = sig;
+    c->mtf_clen = (uint32_t)x;
+    return (uint32_t)x;
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
 constexpr int kMtfAhead = 1;  // symbols whose stamp reads run ahead of the update
@@ -635,7 +654,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
 {
     const uint32_t nb = bt.nblocks;
     // chunk / composition tables: rebuilt and uploaded only when the batch layout changed
-    const uint32_t clen = mtf_chunk_len(c, bt.total);
+    const uint32_t clen = mtf_chunk_len(c, bt);
     const uint64_t sig = layout_sig(2, bt.offs, clen);
     uint32_t nch, nhh, ng, npk;
     if (c->ws_tag[WS_MTF_CHUNKS] == sig) {

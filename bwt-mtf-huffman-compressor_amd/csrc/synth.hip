@@ -200,9 +200,18 @@ void synth_zipf(Ctx *c, uint8_t *d_out, uint64_t nbytes, uint64_t offset)
     uint64_t *d_base = (uint64_t *)(d + o_base);
     uint32_t *d_part = (uint32_t *)(d + o_part);
     uint64_t *d_start = (uint64_t *)(d + o_start);
-    BMH_HIP(hipMemsetAsync(d_base, 0, 8, c->stream));
-    uint64_t h_base = 0;
-    for (uint64_t tok0 = 0;; tok0 += kZipfRound) {
+    // resume from the round the previous call ended in when this window starts at or after it
+    // (a stream generated piece by piece), else from token 0: d_base = bytes before
+    // the first round run
+    uint64_t tok0 = 0, h_base = 0;
+    if (c->zipf_resume_tok0 && offset >= c->zipf_resume_base) {
+        tok0 = c->zipf_resume_tok0;
+        h_base = c->zipf_resume_base;
+    }
+    c->h2d(d_base, &h_base, 8);
+    for (;; tok0 += kZipfRound) {
+        c->zipf_resume_tok0 = tok0;
+        c->zipf_resume_base = h_base;
         BMH_LAUNCH(c, "synth_zipf_count", k_zipf_count, kZipfRoundWG, kZipfNT, 0, d_cdf, d + o_wlen, tok0, d_part);
         BMH_LAUNCH(c, "synth_zipf_scan", k_zipf_scan, 1, 1024, 0, d_part, d_start, d_base);
         BMH_LAUNCH(c, "synth_zipf_write", k_zipf_write, kZipfRoundWG, kZipfNT, 0, d_cdf, (const uint4 *)(d + o_words),

@@ -128,6 +128,9 @@ bmh_status bmh_encode_blocks_dev(bmh_ctx *ctx, const uint8_t *d_in, const uint64
 /* Pipelines (HIP streams, each driven by its own host thread) bmh_encode_blocks_dev runs a batch
  * of nblocks blocks totalling `total` bytes on (the library's rule; BMH_OPT_PIPELINES overrides). */
 uint32_t bmh_encode_pipelines(bmh_ctx *ctx, uint64_t total, uint32_t nblocks);
+/* Pipelines the context's last bmh_encode_blocks_dev call ran on: the rule above, or 1 when a
+ * 32-256 MiB batch's digram census found it dense (uniform-like bytes). */
+uint32_t bmh_ctx_last_pipelines(bmh_ctx *ctx);
 /* Capacity sufficient for one record of an n-byte block. */
 uint64_t bmh_record_bound(uint64_t n);
 

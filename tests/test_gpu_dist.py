@@ -50,11 +50,12 @@ def test_world2_bench_on_gpu(scaling):
     # rank 0 times the reference CPU path at any world size (here on 2 processes to stay short)
     cb = line["cpu_baseline"]
     assert cb is not None and cb["value"] > 0 and cb["cores"] == 2 and cb["kind"] == "reference", cb
-    # the pipelines the library really runs for the rank's batch (capi.cpp stream_count)
-    assert line["config"]["streams_per_gpu"] == 4
+    # the pipelines the library really ran the rank's batch on (capi.cpp encode_blocks): 4 by the
+    # size rule for 512 MiB (strong: 128 blocks a rank), 1 for a dense 256 MiB batch (weak)
+    assert line["config"]["streams_per_gpu"] == (4 if scaling == "strong" else 1)
     if scaling == "strong":
         w = line["weak_scaling"]
-        assert w["bytes_per_gpu"] == 256 << 20 and w["value"] > 0 and w["streams_per_gpu"] == 4
+        assert w["bytes_per_gpu"] == 256 << 20 and w["value"] > 0 and w["streams_per_gpu"] == 1
         assert w["parity"] == "128/128 records byte-identical to the reference manifest", w
     else:
         assert line["weak_scaling"] is None

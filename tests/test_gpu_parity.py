@@ -854,7 +854,8 @@ def _alpha_block(rng, n, k, kind):
 def test_compacted_alphabet_global_pass(ctx, oracle):
     """blocks of k <= 32 distinct bytes key the global pass on s whole symbols
     (s = 3 for k <= 10, 2 for k <= 32; ranks among the block's bytes, db = 8 s) instead of 10 raw
-    bits; their list rounds compare windows of w-bit symbol ranks (12 .. 16 symbols). Boundary
+    bits (only the global pass uses the compacted digits; the record and every later pass stay on
+    raw rotation bits). Boundary
     alphabets (1, 2, 10, 11, 32, 33 distinct bytes), tiny blocks, uniform, word-like and
     deep-repeat text, values spread over the byte range, all in one batch past the run screen's
     batch size (so no block takes the run path): BWT and records equal the oracle's."""
@@ -920,3 +921,31 @@ def test_tuning_options_never_change_records(ctx):
             ctx.set_option(name, 0)
     for opt, v, st in ((99, 1, 1), (1, 17, 4), (4, 5000, 4), (4, 10, 4)):
         assert bmh.lib().bmh_ctx_set_option(ctx.h, opt, v) == st, (opt, v)
+
+
+def test_dense_probe_pipelines(ctx):
+    """encode_blocks' digram census (bwt_runs.hip dense_batch): a 48 MiB batch of random 4 MiB
+    blocks runs on one pipeline, the same size of Zipf text on the size rule's three; records
+    are the reference's either way (random blocks 0..11 of the config-4 manifest)."""
+    bs, nblk = 4 << 20, 12
+    offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
+    d_in = ctx.alloc(bs * nblk)
+    for i in range(nblk):
+        ctx.synth_splitmix64(d_in.ptr.value + i * bs, bs, 0, i * bs)
+    cap = nblk * int(bmh.lib().bmh_record_bound(bs))
+    d_out = ctx.alloc(cap)
+    ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+    assert ctx.last_pipelines() == 1
+    assert ctx.pipelines(bs * nblk, nblk) == 3
+    man = manifest("random_1g_4m")["blocks"]
+    recs = d_out.download(int(ro[-1])).tobytes()
+    for b in range(nblk):
+        assert hashlib.sha256(recs[int(ro[b]):int(ro[b + 1])]).hexdigest() == man[b]["sha256"], b
+    z = synth.zipf_text(bs * nblk)
+    d_in.upload(z)
+    ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+    assert ctx.last_pipelines() == 3
+    ctx.set_option("pipelines", 2)
+    ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+    assert ctx.last_pipelines() == 2
+    ctx.set_option("pipelines", 0)

@@ -6,7 +6,7 @@ the contexts share device 0). The text is the true App. D stream, generated in H
 bmh_synth_zipf_dev and copied to pageable host memory; every record is checked against the
 reference's 512-block manifest (zipf_16m, tests/golden/make_golden.py) and the whole container
 is round-tripped by the GPU decoder (bmh_decompress_dev).
-usage: python tools/config5_run.py [--gib 8] [--contexts 1]"""
+usage: python tools/config5_run.py [--gib 8] [--contexts 1] [--opts name=value,...]"""
 import argparse
 import ctypes as C
 import hashlib
@@ -24,11 +24,14 @@ import bmh  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=int, default=8)
 ap.add_argument("--contexts", type=int, default=1)
+ap.add_argument("--opts", default="", help="bmh_ctx_set_option list name=value,...")
 a = ap.parse_args()
 n = a.gib << 30
 bs = 16 << 20
 L = bmh.lib()
 ctxs = [bmh.Context(0) for _ in range(a.contexts)]
+for c in ctxs:
+    c.set_options(a.opts)
 t0 = time.perf_counter()
 data = np.empty(n, dtype=np.uint8)
 piece = 1 << 30

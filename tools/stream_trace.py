@@ -37,3 +37,17 @@ for sid, kk in sorted(by.items()):
     tops = ", ".join(f"{n} {v:.0f}" for n, v in sorted(top.items(), key=lambda kv: -kv[1])[:5])
     print(f"stream {sid}: {len(kk):4d} launches, {(kk[0][0] - t0) / 1e3:7.1f} .. {(max(k[1] for k in kk) - t0) / 1e3:7.1f} us, "
           f"busy {busy:7.1f} us  [{tops}]")
+
+# union of busy intervals (any stream) and the idle gaps inside the call
+iv = sorted((a, b) for a, b, *_ in c)
+busy, cur_a, cur_b, gaps = 0, iv[0][0], iv[0][1], []
+for a, b in iv[1:]:
+    if a > cur_b:
+        busy += cur_b - cur_a
+        gaps.append((cur_b - t0, a - cur_b))
+        cur_a, cur_b = a, b
+    else:
+        cur_b = max(cur_b, b)
+busy += cur_b - cur_a
+print(f"device busy (union) {busy / 1e3:.1f} us of {(t1 - t0) / 1e3:.1f}; idle gaps > 5 us: " +
+      ", ".join(f"@{g0 / 1e3:.0f}+{g / 1e3:.0f}" for g0, g in gaps if g > 5000))
