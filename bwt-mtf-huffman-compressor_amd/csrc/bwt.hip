@@ -321,8 +321,12 @@ __device__ __forceinline__ void dq_flush(const DataArgs &a, DeferQueue<Q> &q)
 // largest position and R = min(32, 44 - P) (4 MiB blocks: P = 22, R = 22, so one dense
 // finish resolves rotation bits up to 44; rarer deeper ties go to list passes).
 __device__ __forceinline__ uint32_t rec_pbits(uint32_t n) { return n <= 2 ? 1u : 32u - (uint32_t)__builtin_clz(n - 1); }
-// R also keeps db + 12 + R within the 64 rotation bits the global pass reads (db <= 24)
-__device__ __forceinline__ uint32_t rec_rbits(uint32_t P, uint32_t db) { return min(min(32u, 44u - P), 52u - db); }
+// R also keeps db + 12 + R within the 64 rotation bits the global pass reads (db <= 24); a
+// packed record (below) reads no raw window, so only the record's 64 bits bound it
+__device__ __forceinline__ uint32_t rec_rbits(uint32_t P, uint32_t db, bool packed)
+{
+    return packed ? min(32u, 44u - P) : min(min(32u, 44u - P), 52u - db);
+}
 
 // Per-block global-pass alphabet: a block of k <= 32 distinct bytes keys its
 // global pass on s = 2 (k <= 32) or 3 (k <= 10) whole symbols, each replaced by its rank among the
@@ -332,6 +336,37 @@ __device__ __forceinline__ uint32_t rec_rbits(uint32_t P, uint32_t db) { return 
 // lowercase letter has the same top bits); later passes stay in raw bits. info = s | k << 8,
 // 0 for the raw digit (db = kG1Bits).
 __device__ __forceinline__ uint32_t g1_db(uint32_t info) { return info ? 8u * (info & 255u) : kG1Bits; }
+// Packed records: a compacted block's dense-bucket record carries, in place
+// of raw rotation bits [db, db + 12 + R), the w-bit ranks of its next nsym symbols (w = bits of
+// k - 1, left-aligned: order-preserving, since the rank map is monotone), so the dense finish
+// resolves nsym whole symbols (27 letters at 1 MiB blocks: 7 instead of 4.5 characters) and its
+// tied groups go on in raw bits at the whole-symbol depth they reached. kPackSymMax bounds the
+// bytes the global pass reads past each position (its LDS halo).
+constexpr uint32_t kPackSymMax = 12;
+__device__ __forceinline__ uint32_t g1_w(uint32_t info)
+{
+    const uint32_t k = info >> 8;
+    return k <= 1 ? 0u : 32u - (uint32_t)__builtin_clz(k - 1);
+}
+__device__ __forceinline__ uint32_t rec_nsym(uint32_t info, uint32_t R)
+{
+    const uint32_t w = g1_w(info);
+    return w ? min(kPackSymMax, (12u + R) / w) : 0u;
+}
+// Raw bit depths a dense bucket's rotations are known equal to after the finish: dep_dig for a
+// sub-bucket grouped by the 12-bit digit, dep_full after the rest too.
+__device__ __forceinline__ void dense_depths(uint32_t info, uint32_t R, uint32_t &dep_dig, uint32_t &dep_full)
+{
+    const uint32_t db = g1_db(info), ns = info ? rec_nsym(info, R) : 0u;
+    if (ns) {
+        const uint32_t s = info & 255u;
+        dep_dig = 8u * (s + min(ns, kSegDigit / g1_w(info)));
+        dep_full = 8u * (s + ns);
+    } else {
+        dep_dig = db + kSegDigit;
+        dep_full = db + kSegDigit + R;
+    }
+}
 __device__ __forceinline__ uint32_t g1_digit3(uint32_t b0, uint32_t b1, uint32_t b2, uint32_t info, const uint8_t *rk)
 {
     if (!info) return (b0 << (kG1Bits - 8)) | (b1 >> (16 - kG1Bits));
@@ -580,8 +615,9 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
                                                      uint64_t *__restrict__ rec)
 {
     __shared__ uint16_t s_ent[kG1Chunk + 1];  // chunk-relative position (+ a dummy slot)
-    // byte j <-> block position start - 16 + j (cyclic), j < len + 32 (16-byte pieces)
-    __shared__ __align__(16) uint32_t s_txt[(kG1Chunk + 32) / 4];
+    // byte j <-> block position start - 16 + j (cyclic), j < len + 48 (16-byte pieces; a packed
+    // record reads up to 3 + kPackSymMax bytes past a position, as whole dwords)
+    __shared__ __align__(16) uint32_t s_txt[(kG1Chunk + 48) / 4];
     __shared__ uint32_t s_cnt[kG1Bins + 1], s_off[kG1Bins], s_blen[kG1Bins];  // s_off: global - local start
     // (s_cnt[kG1Bins]: sink digit of the slots past the chunk, so the LDS phases run unbranched)
     __shared__ uint32_t s_tmp[17];
@@ -592,6 +628,8 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     const uint32_t t = threadIdx.x;
     const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
     const uint32_t info = a.ainfo[b], db = g1_db(info);
+    // packed records for a compacted block's dense buckets (nsym symbols of wsym bits; 0: raw)
+    const uint32_t nsym = info ? rec_nsym(info, min(32u, 44u - rec_pbits(n))) : 0u, wsym = g1_w(info);
     if (info && t < 256) s_rk[t] = a.arank[(size_t)b * 256 + t];
     const uint8_t *blk = a.data + boff;
     static_assert(kG1Bins <= 1024 && kG1Bits >= 8, "at most one digit per thread");
@@ -606,8 +644,9 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         // 16-byte pieces, all loads in flight before the first LDS store (a load under a
         // per-piece branch waits inside it: one HBM round trip per piece); pieces that wrap
         // around the block or are unaligned take the byte path
-        const uint32_t np = (ch.len + 26 + 15) / 16;  // bytes up to len + 25 are read
-        constexpr uint32_t PPT = (kG1Chunk + 26 + 15) / 16 / 1024 + 1;  // pieces per thread
+        const uint32_t np = (ch.len + 42 + 15) / 16;  // bytes up to len + 41 are read
+        constexpr uint32_t PPT = (kG1Chunk + 42 + 15) / 16 / 1024 + 1;  // pieces per thread
+        static_assert(16 + 3 + kPackSymMax + 3 <= 42 && (kG1Chunk + 42 + 15) / 16 * 16 <= kG1Chunk + 48, "halo");
         uint4 v[PPT];
         bool fast[PPT];
 #pragma unroll
@@ -694,9 +733,26 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
         const uint32_t slot = s_off[d] + i;
         const uint32_t blen = s_blen[d];
         if (blen >= 2 && blen <= kDenseCap) {  // the dense finish reads the record, writes SA
-            // rotation bits [db, db + 12 + R) (key >> 8 holds bits [8, 64))
-            const uint32_t P = rec_pbits(n), R = rec_rbits(P, db);
-            const uint64_t sub = ((key >> 8) >> (52 - db - R)) & ((1ull << (12 + R)) - 1);
+            const uint32_t P = rec_pbits(n), R = rec_rbits(P, db, nsym != 0);
+            uint64_t sub;
+            if (nsym) {
+                // the ranks of symbols s .. s + nsym - 1 (s_txt bytes rel + 16 + s ..), w bits each
+                const uint32_t j1 = rel + 16 + (info & 255u), w1 = j1 >> 2, a1 = j1 & 3u;
+                static_assert(kPackSymMax <= 12, "three aligned dwords");
+                uint32_t dw[4], al[3];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) dw[q] = s_txt[w1 + q];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) al[q] = __builtin_amdgcn_alignbyte(dw[q + 1], dw[q], a1);  // bytes 4q ..
+                uint64_t acc = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kPackSymMax; ++q)
+                    if (q < nsym) acc = (acc << wsym) | s_rk[(al[q >> 2] >> (8 * (q & 3))) & 255u];
+                sub = acc << (12 + R - nsym * wsym);
+            } else {
+                // rotation bits [db, db + 12 + R) (key >> 8 holds bits [8, 64))
+                sub = ((key >> 8) >> (52 - db - R)) & ((1ull << (12 + R)) - 1);
+            }
             rec[boff + slot] = (sub << (P + 8)) | ((uint64_t)p << 8) | (key & 255u);
         } else if (blen > 1 || a.full_sa) {
             a.sa[boff + slot] = p;
@@ -735,8 +791,9 @@ struct FinishShape {
 // and is zero again on return (ends with a barrier); s_tmp holds NT / 64 + 2 words, the last
 // one zero on entry (set when some slot is deferred: then the segment's SA is stored).
 template <uint32_t NT, uint32_t CAP>
-__device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, uint32_t len, uint32_t db, uint32_t b,
-                                            uint32_t R, bool packL, uint32_t (&pl)[FinishShape<NT, CAP>::IPT],
+__device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, uint32_t len, uint32_t dep_dig,
+                                            uint32_t dep_full, uint32_t b, bool packL,
+                                            uint32_t (&pl)[FinishShape<NT, CAP>::IPT],
                                             uint32_t (&dd)[FinishShape<NT, CAP>::IPT],
                                             uint32_t (&rv)[FinishShape<NT, CAP>::IPT], uint32_t *s_rest,
                                             uint32_t *s_cnt, uint32_t *s_tmp, DeferQueue<kDeferQ> &dq)
@@ -782,7 +839,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
     DPROF(3);
     // s_cnt now holds every sub-bucket's end; its start is the previous digit's end. Rank in
     // registers; outputs are parked in LDS at their segment slot and stored in slot order.
-    const uint64_t newbits = (uint64_t)db + kSegDigit + R;
+    const uint64_t newbits = dep_full;
     const bool final_depth = newbits >= 8ull * n;
     // the next element's counter words are read before this element's ranking (one LDS round
     // trip of latency hidden per element)
@@ -806,7 +863,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
         if (m > kSmallM) {
             dd[k] = me;  // deferred, grouped by the 12-bit digit
             if (me == s0) {
-                dq_push(a, dq, gstart + s0, m, db + kSegDigit, b, n);
+                dq_push(a, dq, gstart + s0, m, dep_dig, b, n);
                 s_tmp[NT / 64 + 1] = 1;
             }
             continue;
@@ -1030,7 +1087,8 @@ __device__ __forceinline__ void finish_seg_one(const DataArgs &a, const Seg4 sg,
             }
         }
     }
-    finish_core<NT, CAP>(a, gstart, len, db + cp, b, 32u, false, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+    finish_core<NT, CAP>(a, gstart, len, db + cp + kSegDigit, db + cp + kSegDigit + 32u, b, false, pl, dd, rv, s_rest,
+                         s_cnt, s_tmp, dq);
 }
 
 // one segment per workgroup (grid 8 x the largest lane count from the last wait)
@@ -1298,8 +1356,10 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     const uint32_t t = threadIdx.x;
     DPROF_START;
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
-    const uint32_t db = __builtin_amdgcn_readfirstlane(g1_db(a.ainfo[b]));  // uniform (keeps it out of VGPRs)
-    const uint32_t P = rec_pbits(n), R = __builtin_amdgcn_readfirstlane(rec_rbits(P, db));
+    const uint32_t info = __builtin_amdgcn_readfirstlane(a.ainfo[b]);  // uniform (keeps it out of VGPRs)
+    const uint32_t P = rec_pbits(n), R = __builtin_amdgcn_readfirstlane(rec_rbits(P, g1_db(info), rec_nsym(info, 32u) != 0));
+    uint32_t dep_dig, dep_full;
+    dense_depths(info, R, dep_dig, dep_full);
     const bool packL = P <= 24;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     if (t == 0) s_tmp[NT / 64 + 1] = 0;
@@ -1324,7 +1384,7 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     }
     __syncthreads();
     DPROF(0);
-    finish_core<NT, CAP>(a, boff + e.x, e.y, db, b, R, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
+    finish_core<NT, CAP>(a, boff + e.x, e.y, dep_dig, dep_full, b, packL, pl, dd, rv, s_rest, s_cnt, s_tmp, dq);
 }
 
 // ------------------------------------------------------------- MSD passes on data bits
