@@ -1360,6 +1360,8 @@ __global__ __launch_bounds__(NT) void k_finish_dense(DataArgs a, const uint2 *__
     const uint32_t P = rec_pbits(n), R = __builtin_amdgcn_readfirstlane(rec_rbits(P, g1_db(info), rec_nsym(info, 32u) != 0));
     uint32_t dep_dig, dep_full;
     dense_depths(info, R, dep_dig, dep_full);
+    dep_dig = __builtin_amdgcn_readfirstlane(dep_dig);  // uniform: SGPRs (65 VGPRs cost a workgroup per CU)
+    dep_full = __builtin_amdgcn_readfirstlane(dep_full);
     const bool packL = P <= 24;
     for (uint32_t i = t; i < FinishShape<NT, CAP>::NDIG / 2; i += NT) s_cnt[i] = 0;
     if (t == 0) s_tmp[NT / 64 + 1] = 0;

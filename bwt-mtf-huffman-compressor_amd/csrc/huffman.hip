@@ -28,6 +28,9 @@ constexpr uint32_t kHdrStride = 352;  // 24 header bytes + <= 320 tree bytes, 16
 
 // Phase timing (experiment builds only, -DBMH_PROF_HUFF): lane 0 of each block's wave stores its
 // s_memtime ticks per phase of k_huff_build; codebook_batch prints the means after the launch.
+#ifdef BMH_DEBUG_HUFF
+__device__ uint32_t g_hdbg[8192];  // block 0: per round m, lc, ic, la, ia, bound; then P (lo, hi)
+#endif
 #ifdef BMH_PROF_HUFF
 __device__ uint32_t g_hprof[4096 * 8];
 #define HPROF_START uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -73,14 +76,19 @@ __device__ __forceinline__ uint64_t heap_key(uint64_t freq, uint32_t L, uint32_t
 {
     return (freq << 32) | ((0xffffu - addr_rank(L, id)) << 16) | id;
 }
-// The same for an internal node v >= L, branch-free (addr_rank's chain of cases compiles to a
-// run of scalar branches inside the sequential merge loop): L <= 128: [.., 3..127 -> v - 2, 128..
-// -> v] (v = 2 only for L = 2: rank 127); L > 128: [129..192 -> v - 66, 193.. -> v].
-__device__ __forceinline__ uint64_t heap_key_internal(uint64_t freq, uint32_t L, uint32_t v)
+// A 64-bit value made wave-uniform (two 32-bit reads of lane 0; the builtin returns a signed int,
+// so each half is widened as unsigned — a sign-extended low half would overwrite the high one).
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v)
 {
-    const uint32_t small = L <= 128u;
-    const uint32_t r = small ? (v == 2u ? 127u : v - 2u * (uint32_t)(v <= 127u)) : v - 66u * (uint32_t)(v <= 192u);
-    return (freq << 32) | ((0xffffu - r) << 16) | v;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// The closed-form address rank of internal node v >= L (ascending with v).
+__device__ __forceinline__ uint32_t internal_rank(uint32_t L, uint32_t v)
+{
+    return L <= 128u ? (v == 2u ? 127u : v - 2u * (uint32_t)(v <= 127u)) : v - 66u * (uint32_t)(v <= 192u);
 }
 
 // Rank of each of this lane's keys (slots lane + 64k) among the 256 keys of s_keys (padding
@@ -121,8 +129,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ uint16_t s_dep[512];                    // path length to the jump target
     __shared__ uint64_t s_pcode[512];                  // path bits to the jump target (left 0, right 1)
     __shared__ uint64_t s_lkey[256];                   // leaf keys, then left-aligned leaf codes
-    __shared__ uint64_t s_k1[256], s_q2[256];          // leaves in pop order; internal-node queue
-    __shared__ uint16_t s_gs[256];                     // internal-node queue: group start slots
+    __shared__ uint64_t s_k1[256], s_q2[512];          // leaves in pop order; the pop sequence P
     __shared__ uint32_t s_err;
     uint8_t *s_tree = (uint8_t *)s_tree32;
     const uint32_t b = blockIdx.x, lane = threadIdx.x;
@@ -209,16 +216,21 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 if (lane + 64 * k == v) key[k] = (f << 9) | (511u - rkr[k]);
         }
     } else {
-        // (A wave-uniform form of this loop, queues in registers read by v_readlane with 64-bit keys
-        // moved as two halves, measured slower: 437 K vs 289 K ticks of merges for Calgary's
-        // blocks, profiles/r04/huff_build_ab_v1.txt — the selects and hazards of the register
-        // reads cost more than the LDS reads they replace. Round 3's wave-uniform attempt failed
-        // for another reason: its u64 keys went through a 32-bit readfirstlane)
-        // the priority queue (main.cpp:245-254): first pop -> left child, second -> right. Run as
-        // two queues: the leaves sorted by key, and the internal nodes, which are created with
-        // non-decreasing frequencies and ascending address ranks; so the queue of internal nodes is
-        // a run of frequency groups, each popped newest first (the larger rank of an equal
-        // frequency pops first). Exactly the heap's pop order, O(1) per pop, on lane 0.
+        // The reference's priority queue (main.cpp:245-254: first pop -> left child, second ->
+        // right) in parallel rounds. A new node's frequency is the sum of the two it was made from,
+        // so it exceeds the frequency of everything popped so far, and its key is larger than
+        // every popped key: the pops come out in ascending key order, i.e. the pop sequence P is
+        // the sorted sequence of all non-root node keys, and internal node j (id L + j) is made
+        // of P[2j] and P[2j + 1]. Internal frequencies F[j] never decrease with j and their
+        // address ranks ascend with j, so the internal keys sort by F, newest first among equals.
+        // A round takes the known nodes 0 .. m-1: every node made later has a key >= B = (F[m-1],
+        // the largest internal rank), so all known items below B are the smallest |D| items of P;
+        // they are merged into P (two sorted runs, the leaves and the internals of complete
+        // frequency groups), and every node j with 2j + 1 < |D| is made at once. When that is no
+        // progress (a chain where each new node is popped next), the round pops the two smallest
+        // remaining items as the heap would. Random data takes ~10 rounds, text and Calgary
+        // 15-27, instead of L - 1 sequential merges (tests/test_huffman_queue.py restates it).
+        // leaf keys (frequency, descending address rank, id), sorted into s_k1
         for (uint32_t id = lane; id < 256; id += 64) s_lkey[id] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
         __syncthreads();
         {
@@ -230,71 +242,112 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         }
         __syncthreads();
         HPROF(5);  // (model path) leaf keys ranked
-        if (lane == 0) {
-            uint32_t q1 = 0;                          // next leaf
-            uint32_t gh = 0, ge = 0, gn = 0, me = 0;  // first group [gh, ge) (+ popped slots up to gn); slots end at me
-            // queue heads kept in registers with the entries behind them, their LDS reads issued
-            // two pops ahead of use: k1 = s_k1[q1], k1n = s_k1[q1 + 1], k1m = s_k1[q1 + 2]; k2 =
-            // s_q2[ge - 1], k2b = s_q2[ge - 2] while that is still in the first group (else ~0)
-            uint64_t k1 = s_k1[0], k1n = L > 1 ? s_k1[1] : ~0ull, k1m = L > 2 ? s_k1[2] : ~0ull;
-            uint64_t k2 = ~0ull, k2b = ~0ull;
-            uint32_t gf = 0, lf = 0;  // first group's frequency; the last slot's
-            // start slots of the groups after the first, in order (gq = the next one's entry): a
-            // group's end is the next start, no scan over its slots
-            uint32_t gq = 0, ngs = 0;
-            auto pop = [&]() -> uint64_t {
-                uint64_t r;
-                if (k1 < k2) {
-                    r = k1;
-                    ++q1;
-                    k1 = k1n;
-                    k1n = k1m;
-                    k1m = q1 + 2 < L ? s_k1[q1 + 2] : ~0ull;
-                } else {
-                    r = k2;
-                    --ge;
-                    if (ge > gh) {
-                        k2 = k2b;
-                        k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
-                    } else {  // the first group is used up: the next one starts at gn
-                        gh = gn;
-                        ge = gh;
-                        k2 = ~0ull;
-                        k2b = ~0ull;
-                        if (gh < me) {
-                            ++gq;  // s_gs[gq - 1] == gh
-                            ge = gq < ngs ? (uint32_t)s_gs[gq] : me;
-                            gn = ge;
-                            k2 = s_q2[ge - 1];
-                            k2b = ge - 1 > gh ? s_q2[ge - 2] : ~0ull;
-                            gf = (uint32_t)(k2 >> 32);
-                        }
-                    }
+        uint64_t *s_P = s_q2;          // P (keys), 2 L - 2 entries
+        uint64_t *s_IK = s_pcode;      // sorted internal keys (s_pcode is free until the codes)
+        __shared__ uint32_t s_F[256];  // F[j]
+        const uint32_t rmax = internal_rank(L, 2 * L - 2);
+        uint64_t lkr[4];  // sorted leaf keys, slot lane + 64 k
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lkr[k] = lane + 64 * k < L ? s_k1[lane + 64 * k] : ~0ull;
+        uint32_t fr[4] = {~0u, ~0u, ~0u, ~0u};  // F of node lane + 64 k (nodes < m)
+        uint64_t gm[4] = {0, 0, 0, 0};          // group starts among nodes 0 .. m-1 (uniform)
+        uint32_t m = 0, lc = 0, ic = 0;         // known nodes; leaves / internals placed in P
+        // sorted internal index x -> node: x's frequency group [gs, ge) reversed
+        auto node_of = [&](uint32_t x) -> uint32_t {
+            uint32_t q = x >> 6;
+            uint64_t w = gm[q] & (((2ull << (x & 63u)) - 1) | ((x & 63u) == 63u ? ~0ull : 0ull));
+            for (uint32_t t = 0; t < 3 && !w && q > 0; ++t) w = gm[--q];
+            const uint32_t gs = 64 * q + 63 - (uint32_t)__builtin_clzll(w);
+            q = x >> 6;
+            w = (x & 63u) == 63u ? 0ull : gm[q] & ~((2ull << (x & 63u)) - 1);
+            for (uint32_t t = 0; t < 3 && !w && q < 3; ++t) w = gm[++q];
+            const uint32_t ge = w ? 64 * q + (uint32_t)__builtin_ctzll(w) : m;
+            return gs + ge - 1 - x;
+        };
+        auto ikey = [&](uint32_t j) -> uint64_t {
+            return ((uint64_t)s_F[j] << 32) | ((uint64_t)(0xffffu - internal_rank(L, L + j)) << 16) | (L + j);
+        };
+        // first index in [lo, hi) of the sorted array a whose key is >= x
+        auto lower = [&](const uint64_t *a, uint32_t lo, uint32_t hi, uint64_t x) -> uint32_t {
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (a[mid] < x) lo = mid + 1;
+                else hi = mid;
+            }
+            return lo;
+        };
+        for (uint32_t guard = 0; m + 1 < L && guard < L; ++guard) {  // m grows every round
+            uint32_t la = 0, ia = 0;
+            bool bound = false;
+            if (m > 0) {
+                const uint32_t fm1 = __builtin_amdgcn_readfirstlane(s_F[m - 1]);
+                const uint64_t B = ((uint64_t)fm1 << 32) | ((uint64_t)(0xffffu - rmax) << 16);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    la += (uint32_t)__builtin_popcountll(__ballot(lkr[k] < B));
+                    ia += (uint32_t)__builtin_popcountll(__ballot(lane + 64u * k < m && fr[k] < fm1));
                 }
-                return r;
-            };
-            for (uint32_t m = 0; m + 1 < L; ++m) {
-                const uint64_t ra = pop(), rb = pop();
-                const uint32_t v = L + m;
-                const uint64_t f = (ra >> 32) + (rb >> 32);
-                s_left[v] = (int16_t)(ra & 0xffffu);
-                s_right[v] = (int16_t)(rb & 0xffffu);
-                const uint64_t nk = heap_key_internal(f, L, v);
-                if (gn == me && (ge == gh || (uint32_t)f == gf)) {
-                    // the queue is empty, or the node joins the last (= first) group: it pops first
-                    if (ge == gh) gf = (uint32_t)f;
-                    k2b = ge == gh ? ~0ull : k2;  // the old head is now the second
-                    s_q2[ge++] = nk;
-                    if (ge > gn) gn = me = ge;
-                    k2 = nk;
-                } else {
-                    // a later group: a new one unless it has the last slot's frequency
-                    if (gn == me || (uint32_t)f != lf) s_gs[ngs++] = (uint16_t)me;
-                    s_q2[me++] = nk;
+                bound = la + ia >= 2 * m + 2;
+            }
+#ifdef BMH_DEBUG_HUFF
+            if (b == 0 && lane == 0 && guard < 256) {
+                uint32_t *g = g_hdbg + 8 * guard;
+                g[0] = m; g[1] = lc; g[2] = ic; g[3] = la; g[4] = ia; g[5] = bound; g[6] = L; g[7] = 0xabcd;
+            }
+#endif
+            if (bound) {
+                for (uint32_t x = ic + lane; x < ia; x += 64) s_IK[x] = ikey(node_of(x));
+                __syncthreads();
+                const uint32_t base = lc + ic;
+                for (uint32_t i = lc + lane; i < la; i += 64) {
+                    const uint64_t key = s_k1[i];
+                    s_P[base + (i - lc) + (lower(s_IK, ic, ia, key) - ic)] = key;
                 }
-                lf = (uint32_t)f;
+                for (uint32_t x = ic + lane; x < ia; x += 64) {
+                    const uint64_t key = s_IK[x];
+                    s_P[base + (x - ic) + (lower(s_k1, lc, la, key) - lc)] = key;
+                }
+                lc = la;
+                ic = ia;
+            } else {
+                // the smallest remaining items (the heads of the two sorted runs), uniformly, up to
+                // P[2m + 1] (P[2m] may be placed already)
+                while (lc + ic < 2 * m + 2) {
+                    const uint64_t a = lc < L ? s_k1[lc] : ~0ull;
+                    uint64_t c = ~0ull;
+                    if (ic < m) c = ikey(node_of(ic));
+                    const uint64_t au = uniform_u64(a), cu = uniform_u64(c);
+                    s_P[lc + ic] = au < cu ? au : cu;  // every lane stores the same value
+                    if (au < cu) ++lc;
+                    else ++ic;
+                }
+            }
+            __syncthreads();
+            const uint32_t m2 = min((lc + ic) / 2, L - 1);
+            for (uint32_t j = m + lane; j < m2; j += 64) {
+                const uint64_t a = s_P[2 * j], c = s_P[2 * j + 1];
+                s_left[L + j] = (int16_t)(a & 0xffffu);
+                s_right[L + j] = (int16_t)(c & 0xffffu);
+                s_F[j] = (uint32_t)(a >> 32) + (uint32_t)(c >> 32);
+            }
+            __syncthreads();
+            m = m2;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t j = lane + 64u * k;
+                fr[k] = j < m ? s_F[j] : ~0u;
+                const bool st = j < m && (j == 0 || s_F[j - 1] != fr[k]);
+                gm[k] = __ballot(st);
             }
         }
+#ifdef BMH_DEBUG_HUFF
+        __syncthreads();
+        if (b == 0)
+            for (uint32_t x = lane; x < 2 * L - 2; x += 64) {
+                g_hdbg[2048 + 2 * x] = (uint32_t)s_P[x];
+                g_hdbg[2048 + 2 * x + 1] = (uint32_t)(s_P[x] >> 32);
+            }
+#endif
     }
     __syncthreads();
     HPROF(1);  // the queue (merges; key ranking too on the heap-history path)
@@ -522,6 +575,21 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
     }
     BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
                d_status, d_rbase, d_ridx, d_rrank);
+#ifdef BMH_DEBUG_HUFF
+    {
+        std::vector<uint32_t> h(8192);
+        BMH_HIP(hipStreamSynchronize(c->stream));
+        BMH_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_hdbg), h.size() * 4));
+        fprintf(stderr, "huff dbg rounds:");
+        for (int r = 0; r < 256 && h[8 * r + 7] == 0xabcd; ++r)
+            fprintf(stderr, " [m%u lc%u ic%u la%u ia%u b%u]", h[8 * r], h[8 * r + 1], h[8 * r + 2], h[8 * r + 3], h[8 * r + 4], h[8 * r + 5]);
+        fprintf(stderr, "\nhuff dbg P:");
+        const uint32_t L = h[6];
+        for (uint32_t x = 0; x + 2 < 2 * L; ++x)
+            fprintf(stderr, " %u:%u", h[2048 + 2 * x + 1], h[2048 + 2 * x] & 0xffffu);
+        fprintf(stderr, "\n");
+    }
+#endif
 #ifdef BMH_PROF_HUFF
     {
         std::vector<uint32_t> h(4096 * 8);

@@ -1,8 +1,12 @@
-"""The two-queue form of the reference's Huffman priority queue (main.cpp:245-254), as
-k_huff_build's lane-0 loop runs it (csrc/huffman.hip: sorted leaves; internal nodes in frequency
-groups popped newest first, the group starts kept in a FIFO), restated in Python and checked
-against the oracle's tree, on real blocks and on random frequency vectors full of ties; and the
-diagnosis of round 3's failed wave-uniform attempt
+"""The reference's Huffman priority queue (main.cpp:245-254) restated two ways and checked against
+the oracle's trees, on real blocks and on random frequency vectors full of ties:
+  * the two-queue form round 4's k_huff_build ran on one lane (sorted leaves; internal nodes in
+    frequency groups popped newest first, the group starts kept in a FIFO);
+  * the parallel rounds k_huff_build runs now (csrc/huffman.hip, round 5): the pop sequence is the
+    sorted sequence of all non-root keys, so each round merges every item known to lie below the
+    smallest key a later node can have and makes every node whose two children are then known,
+    with a heap-order step (the two smallest remaining items) when that makes no progress.
+And the diagnosis of round 3's failed wave-uniform attempt
 (VERDICT r3 item 5): with the 64-bit queue keys (frequency << 32 | address rank | id) read
 through a 32-bit cross-lane read (readfirstlane of a u64 keeps the low half), the merges order
 nodes by address rank alone, and zipf n = 39,800 encodes to exactly the 30,932-byte record that
@@ -100,6 +104,75 @@ def two_queue_lengths(freq: np.ndarray, first: np.ndarray, key_bits: int = 64):
     return order, [depth[i] for i in range(L)], fr
 
 
+def _internal_rank(L: int, v: int) -> int:
+    # huffman.hip internal_rank: the closed-form rank of internal node v >= L (ascending in v)
+    if L <= 128:
+        return 127 if v == 2 else (v - 2 if v <= 127 else v)
+    return v - 66 if v <= 192 else v
+
+
+def parallel_rounds_lengths(freq: np.ndarray, first: np.ndarray):
+    """Code lengths per leaf (first-occurrence order) and the number of rounds, from the round
+    form k_huff_build runs (bound rounds and heap-order steps, as in the kernel)."""
+    import bisect
+    order = sorted((s for s in range(256) if freq[s]), key=lambda s: first[s])
+    L = len(order)
+    if L == 1:
+        return order, [0], 0
+    A = sorted((int(freq[order[i]]) << 32) | ((0xFFFF - _addr_rank(L, i)) << 16) | i for i in range(L))
+    F, kids, P = [], {}, []
+    rmax = _internal_rank(L, 2 * L - 2)
+
+    def ikey(j):
+        return (F[j] << 32) | ((0xFFFF - _internal_rank(L, L + j)) << 16) | (L + j)
+
+    def sorted_internals(m):
+        # sorted internal index x -> node: frequency groups reversed (newest first)
+        out, j = [], 0
+        while j < m:
+            e = j
+            while e < m and F[e] == F[j]:
+                e += 1
+            out += list(range(e - 1, j - 1, -1))
+            j = e
+        return out
+
+    m = lc = ic = rounds = 0
+    while m + 1 < L:
+        rounds += 1
+        srt = sorted_internals(m)
+        bound = False
+        if m:
+            B = (F[m - 1] << 32) | ((0xFFFF - rmax) << 16)
+            la = bisect.bisect_left(A, B)
+            ia = sum(1 for j in range(m) if F[j] < F[m - 1])
+            bound = la + ia >= 2 * m + 2
+        if bound:
+            new = sorted(A[lc:la] + [ikey(srt[x]) for x in range(ic, ia)])
+            P[lc + ic:] = new
+            lc, ic = la, ia
+        else:
+            while lc + ic < 2 * m + 2:
+                a = A[lc] if lc < L else 1 << 64
+                c = ikey(srt[ic]) if ic < m else 1 << 64
+                P[lc + ic:lc + ic + 1] = [min(a, c)]
+                if a < c:
+                    lc += 1
+                else:
+                    ic += 1
+        m2 = min((lc + ic) // 2, L - 1)
+        for j in range(m, m2):
+            a, c = P[2 * j], P[2 * j + 1]
+            F.append((a >> 32) + (c >> 32))
+            kids[L + j] = (a & 0xFFFF, c & 0xFFFF)
+        m = m2
+    depth = {2 * L - 2: 0}
+    for v in range(2 * L - 2, L - 1, -1):
+        for c in kids[v]:
+            depth[c] = depth[v] + 1
+    return order, [depth[i] for i in range(L)], rounds
+
+
 def record_len(freq, first, key_bits=64) -> int:
     order, dep, fr = two_queue_lengths(freq, first, key_bits)
     L = len(order)
@@ -133,6 +206,44 @@ def test_two_queue_matches_oracle_on_tied_frequencies(oracle):
         order, dep, _ = two_queue_lengths(freq, first)
         oln, _, _ = oracle.huffman_build(freq, first)
         assert [int(oln[s]) for s in order] == dep, (trial, L, hi)
+
+
+def test_parallel_rounds_match_oracle_tree(oracle):
+    """The round form k_huff_build runs (round 5) against the oracle's trees: real blocks (random,
+    Zipf, Calgary text / binary / pic) and the tied random vectors of every alphabet class; the
+    rounds stay far below the L - 1 sequential merges."""
+    for data in (synth.zipf_text(300_000).tobytes(), synth.splitmix64_bytes(0, 0, 200_000).tobytes(),
+                 open(os.path.join(GOLDEN, "calgary", "paper1"), "rb").read(),
+                 open(os.path.join(GOLDEN, "calgary", "pic"), "rb").read()[:200_000],
+                 open(os.path.join(GOLDEN, "calgary", "obj1"), "rb").read()):
+        _, L_ = oracle.bwt(data)
+        freq, first = oracle.histogram(oracle.mtf(L_))
+        order, dep, rounds = parallel_rounds_lengths(freq, first)
+        oln, _, _ = oracle.huffman_build(freq, first)
+        assert [int(oln[s]) for s in order] == dep
+        assert rounds <= 30, (rounds, len(order))
+    rng = np.random.default_rng(11)
+    for trial in range(300):
+        L = int(rng.choice([1, 2, 3, 5, 17, 64, 127, 128, 129, 130, 200, 255, 256]))
+        hi = int(rng.choice([1, 2, 3, 5, 40, 1000]))
+        freq = np.zeros(256, np.uint32)
+        syms = rng.choice(256, L, replace=False)
+        freq[syms] = rng.integers(1, hi + 1, L)
+        first = np.full(256, 0xFFFFFFFF, np.uint32)
+        first[syms] = rng.permutation(L * 7)[:L]
+        order, dep, _ = parallel_rounds_lengths(freq, first)
+        oln, _, _ = oracle.huffman_build(freq, first)
+        assert [int(oln[s]) for s in order] == dep, (trial, L, hi)
+    # a Fibonacci chain: every new node is popped next, so every round is a heap-order step
+    fib = [1, 1]
+    while len(fib) < 40:
+        fib.append(fib[-1] + fib[-2])
+    freq = np.zeros(256, np.uint64)
+    freq[:40] = fib
+    first = np.arange(256, dtype=np.uint64)
+    order, dep, rounds = parallel_rounds_lengths(freq, first)
+    oln, _, _ = oracle.huffman_build(freq, first)
+    assert [int(oln[s]) for s in order] == dep
 
 
 def test_round3_wave_uniform_defect_reproduced(oracle):
