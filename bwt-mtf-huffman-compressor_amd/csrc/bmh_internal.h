@@ -75,7 +75,7 @@ struct Ctx {
     // overwritten; get() clears it on reallocation) and a few counts derived with it, so a
     // batch with the same layout as the previous one skips the rebuild and the upload
     uint64_t ws_tag[WS_COUNT_] = {};
-    uint32_t ws_aux[WS_COUNT_][4] = {};
+    uint32_t ws_aux[WS_COUNT_][6] = {};
     // pinned host staging
     void *pinned = nullptr;
     size_t pinned_size = 0;

@@ -568,9 +568,10 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
     const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // list indices c0 + 8k (XCD lane stride)
-    // two sweeps over the block's chunk counts (8 loads in flight each): the digit's total,
-    // then, after the block scan, each chunk's write offset
-    constexpr uint32_t U = 8;
+    // two sweeps over the block's chunk counts (32 loads in flight each: a small batch's few
+    // workgroups are latency-bound here): the digit's total, then, after the block scan, each
+    // chunk's write offset
+    constexpr uint32_t U = 32;
     auto at = [&](uint32_t k) -> uint32_t & { return chist[(size_t)(c0 + 8 * k) * kG1Bins + d]; };
     uint32_t run = 0;
     for (uint32_t k = 0; k < nc; k += U) {

@@ -28,9 +28,6 @@ constexpr uint32_t kHdrStride = 352;  // 24 header bytes + <= 320 tree bytes, 16
 
 // Phase timing (experiment builds only, -DBMH_PROF_HUFF): lane 0 of each block's wave stores its
 // s_memtime ticks per phase of k_huff_build; codebook_batch prints the means after the launch.
-#ifdef BMH_DEBUG_HUFF
-__device__ uint32_t g_hdbg[8192];  // block 0: per round m, lc, ic, la, ia, bound; then P (lo, hi)
-#endif
 #ifdef BMH_PROF_HUFF
 __device__ uint32_t g_hprof[4096 * 8];
 #define HPROF_START uint64_t _t0 = __builtin_amdgcn_s_memtime()
@@ -289,12 +286,6 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 }
                 bound = la + ia >= 2 * m + 2;
             }
-#ifdef BMH_DEBUG_HUFF
-            if (b == 0 && lane == 0 && guard < 256) {
-                uint32_t *g = g_hdbg + 8 * guard;
-                g[0] = m; g[1] = lc; g[2] = ic; g[3] = la; g[4] = ia; g[5] = bound; g[6] = L; g[7] = 0xabcd;
-            }
-#endif
             if (bound) {
                 for (uint32_t x = ic + lane; x < ia; x += 64) s_IK[x] = ikey(node_of(x));
                 __syncthreads();
@@ -340,14 +331,6 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 gm[k] = __ballot(st);
             }
         }
-#ifdef BMH_DEBUG_HUFF
-        __syncthreads();
-        if (b == 0)
-            for (uint32_t x = lane; x < 2 * L - 2; x += 64) {
-                g_hdbg[2048 + 2 * x] = (uint32_t)s_P[x];
-                g_hdbg[2048 + 2 * x + 1] = (uint32_t)(s_P[x] >> 32);
-            }
-#endif
     }
     __syncthreads();
     HPROF(1);  // the queue (merges; key ranking too on the heap-history path)
@@ -575,21 +558,6 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
     }
     BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
                d_status, d_rbase, d_ridx, d_rrank);
-#ifdef BMH_DEBUG_HUFF
-    {
-        std::vector<uint32_t> h(8192);
-        BMH_HIP(hipStreamSynchronize(c->stream));
-        BMH_HIP(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_hdbg), h.size() * 4));
-        fprintf(stderr, "huff dbg rounds:");
-        for (int r = 0; r < 256 && h[8 * r + 7] == 0xabcd; ++r)
-            fprintf(stderr, " [m%u lc%u ic%u la%u ia%u b%u]", h[8 * r], h[8 * r + 1], h[8 * r + 2], h[8 * r + 3], h[8 * r + 4], h[8 * r + 5]);
-        fprintf(stderr, "\nhuff dbg P:");
-        const uint32_t L = h[6];
-        for (uint32_t x = 0; x + 2 < 2 * L; ++x)
-            fprintf(stderr, " %u:%u", h[2048 + 2 * x + 1], h[2048 + 2 * x] & 0xffffu);
-        fprintf(stderr, "\n");
-    }
-#endif
 #ifdef BMH_PROF_HUFF
     {
         std::vector<uint32_t> h(4096 * 8);

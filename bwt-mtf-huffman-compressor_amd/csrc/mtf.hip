@@ -84,15 +84,19 @@ struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
 };
 
-// One wave per chunk (four per workgroup, no workgroup barriers), lane l owns positions
-// [64l, 64l + 64) loaded as one 64-byte sector. R[c][0..d) = distinct symbols, most recent last
-// occurrence first: LDS atomicMax of positions, a bitset of last-occurrence positions, then each
-// set bit's rank = set bits above it (wave scan).
+// One wave per chunk (four per workgroup, no workgroup barriers). The chunk is spread over all 64
+// lanes (lane l reads `span` bytes from span * l, span = len / 64 rounded up to whole dwords), so
+// a short chunk (1408 symbols for a 128 MiB batch) costs its length, not a 4096-symbol walk on a
+// third of the lanes. R[c][0..d) = distinct symbols, most recent last occurrence first: LDS
+// atomicMax of positions, a bitset of last-occurrence positions (lane l owns the 64 positions
+// from 64l), then each symbol's rank = set bits above its last position (wave scan + one
+// popcount), and the symbol is stored at its rank.
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                      uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
 {
     __shared__ int lastpos[4][256];
     __shared__ uint32_t bset[4][kMtfChunk / 32];
+    __shared__ uint32_t above[4][64];
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u, c = blockIdx.x * 4 + w;
     if (c >= nch) return;  // the whole wave
     const MChunk ch = chunks[c];
@@ -101,26 +105,29 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
     bset[w][2 * l] = 0;
     bset[w][2 * l + 1] = 0;
     uint32_t sw[16];
-    const uint32_t e0 = 64 * l;
-    const uint32_t nv = e0 < ch.len ? min(64u, ch.len - e0) : 0u;
-    if (nv == 64 && ((ch.start + e0) & 15u) == 0) {
-        const uint4 *p = (const uint4 *)(L + ch.start + e0);
+    const uint32_t span = (((ch.len + 63) >> 6) + 3) & ~3u;  // <= 64
+    const uint32_t e0 = span * l;
+    const uint32_t nv = e0 < ch.len ? min(span, ch.len - e0) : 0u;
+    const uint8_t *src = L + ch.start + e0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 v = p[q];
-            sw[4 * q] = v.x;
-            sw[4 * q + 1] = v.y;
-            sw[4 * q + 2] = v.z;
-            sw[4 * q + 3] = v.w;
+    for (int q = 0; q < 16; ++q) sw[q] = 0;
+    if ((ch.start & 3u) == 0) {
+        const uint32_t fd = nv >> 2;  // whole dwords (aligned: span and start are multiples of 4)
+#pragma unroll
+        for (uint32_t q = 0; q < 16; ++q)
+            if (q < fd) sw[q] = ((const uint32_t *)src)[q];
+        for (uint32_t k = 4 * fd; k < nv; ++k) {
+            const uint32_t x = (uint32_t)src[k] << (8 * (k & 3));
+#pragma unroll
+            for (uint32_t q = 0; q < 16; ++q)
+                if (q == (k >> 2)) sw[q] |= x;
         }
     } else {
-#pragma unroll
-        for (int q = 0; q < 16; ++q) sw[q] = 0;
         for (uint32_t k = 0; k < nv; ++k) {
-            const uint32_t x = (uint32_t)L[ch.start + e0 + k] << (8 * (k & 3));
+            const uint32_t x = (uint32_t)src[k] << (8 * (k & 3));
 #pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if ((uint32_t)q == (k >> 2)) sw[q] |= x;
+            for (uint32_t q = 0; q < 16; ++q)
+                if (q == (k >> 2)) sw[q] |= x;
         }
     }
     wave_sync();
@@ -129,22 +136,27 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
         if (k < nv) atomicMax(&lastpos[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
     wave_sync();
     uint32_t d = 0;
+    int lp[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int lp = lastpos[w][4 * l + k];
-        if (lp >= 0) atomicOr(&bset[w][lp >> 5], 1u << (lp & 31));
-        d += lp >= 0;
+        lp[k] = lastpos[w][4 * l + k];
+        if (lp[k] >= 0) atomicOr(&bset[w][lp[k] >> 5], 1u << (lp[k] & 31));
+        d += lp[k] >= 0;
     }
     wave_sync();
     d = wave_sum_dpp(d);
     const uint64_t v = ((uint64_t)bset[w][2 * l + 1] << 32) | bset[w][2 * l];
     const uint32_t cnt = (uint32_t)__builtin_popcountll(v);
-    const uint32_t inc = wave_incl_sum_dpp(cnt);
-    uint32_t off = d - inc;  // set bits in lanes above this one
+    above[w][l] = d - wave_incl_sum_dpp(cnt);  // set bits in lanes above this one
+    wave_sync();
     uint8_t *Rc = R + (size_t)c * 256;
 #pragma unroll
-    for (int b = 63; b >= 0; --b)
-        if ((v >> b) & 1u) Rc[off++] = (uint8_t)(sw[b >> 2] >> (8 * (b & 3)));
+    for (int k = 0; k < 4; ++k)
+        if (lp[k] >= 0) {
+            const uint32_t ol = (uint32_t)lp[k] >> 6, b = (uint32_t)lp[k] & 63u;
+            const uint64_t ov = ((uint64_t)bset[w][2 * ol + 1] << 32) | bset[w][2 * ol];
+            Rc[above[w][ol] + (uint32_t)__builtin_popcountll((ov >> b) >> 1)] = (uint8_t)(4 * l + k);
+        }
     if (l == 0) dcount[c] = d;
 }
 
@@ -161,6 +173,7 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
 // ahead into registers and parked in LDS, so the sequential chain never waits on memory.
 constexpr uint32_t kComposeBatch = 32;
 constexpr uint32_t kSuper = 32;  // chunks per superchunk
+constexpr uint32_t kFiveLevel = 1024;  // chunks per block past which the composition takes five levels
 
 struct CRun {
     uint32_t c0, c1;  // list indices [c0, c1)
@@ -577,19 +590,30 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
     if (t < kFirstBmWords) s_bm[t] = 0;
     if (t < 256) {
         f[t] = 0xffffffffu;
-        uint32_t cv = 0xffffffffu;  // first chunk holding t (block-relative); none for absent values
-        bool look = freq[(size_t)b * 256 + t] != 0;
-        for (uint32_t base = 0; look && base < nc; base += 16) {
+        s_cv[t] = 0xffffffffu;  // first chunk holding t (block-relative); none for absent values
+    }
+    __syncthreads();
+    {
+        // value v = t & 255 searched by 4 threads, thread q over the chunk groups 16 q + 64 i:
+        // a value first seen late in a long block (Calgary's text files: ~200 chunks) costs a
+        // quarter of the dependent load rounds; each thread stops at its first hit
+        const uint32_t v = t & 255u, q = t >> 8;
+        bool look = freq[(size_t)b * 256 + v] != 0;
+        for (uint32_t base = 16 * q; look && base < nc; base += 64) {
             uint32_t cnt[16];
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + t] : 0u;
+            for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + v] : 0u;
+            uint32_t cv = 0xffffffffu;
 #pragma unroll
             for (int j = 15; j >= 0; --j)
                 if (cnt[j]) cv = base + j;
-            look = cv == 0xffffffffu;
+            if (cv != 0xffffffffu) {
+                atomicMin(&s_cv[v], cv);
+                look = false;
+            }
         }
-        s_cv[t] = cv;
     }
+    static_assert(kFirstNT == 1024, "k_mtf_first: four searching threads per value");
     __syncthreads();
     if (bitmap) {
         if (t < 256 && s_cv[t] != 0xffffffffu) atomicOr(&s_bm[s_cv[t] >> 5], 1u << (s_cv[t] & 31u));
@@ -656,12 +680,13 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     // chunk / composition tables: rebuilt and uploaded only when the batch layout changed
     const uint32_t clen = mtf_chunk_len(c, bt);
     const uint64_t sig = layout_sig(2, bt.offs, clen);
-    uint32_t nch, nhh, ng, npk;
+    uint32_t nch, nhh, ng, npk, ng2;
     if (c->ws_tag[WS_MTF_CHUNKS] == sig) {
         nch = c->ws_aux[WS_MTF_CHUNKS][0];
         nhh = c->ws_aux[WS_MTF_CHUNKS][1];
         ng = c->ws_aux[WS_MTF_CHUNKS][2];
         npk = c->ws_aux[WS_MTF_CHUNKS][3];
+        ng2 = c->ws_aux[WS_MTF_CHUNKS][4];
     } else {
         std::vector<MChunk> hc;
         std::vector<HChunk> hh;
@@ -688,14 +713,23 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                 hh.push_back(HChunk{b, (uint32_t)(o + s), (uint32_t)std::min<uint64_t>(65536, n - s), (uint32_t)s});
         }
         cfirst[nb] = (uint32_t)hc.size();
-        // composition runs: superchunks of `sup` chunks (levels 1 and 3), blocks (level 2); the
-        // sequential walks are sup and chunks / sup steps long, so short chunks (more of them
-        // per block) take superchunks of ~sqrt(chunks per block), at least kSuper
+        // composition runs. Three levels (kSuper-chunk superchunks composed, the block walks its
+        // superchunk lists, each superchunk walks its chunk lists) cost sup + chunks / sup + sup
+        // sequential steps; blocks of more than kFiveLevel chunks (short chunks of small
+        // batches) add a middle level: groups of s superchunks composed, the block walks the
+        // group lists, each group walks its superchunk lists — five walks of ~cbrt(chunks per
+        // block) steps each (a 128 MiB batch's 2980-chunk blocks: 74 steps instead of 166).
         uint32_t cpb = 1;
         for (uint32_t b = 0; b < nb; ++b) cpb = std::max(cpb, cfirst[b + 1] - cfirst[b]);
-        uint32_t sup = kSuper;
-        while (sup * sup < cpb) sup += 8;
-        std::vector<CRun> r1, r2, r3;
+        uint32_t sup = kSuper, s2 = 0;
+        if (cpb > kFiveLevel) {
+            sup = 8;
+            while (sup * sup * sup < cpb) ++sup;
+            s2 = sup;
+        } else {
+            while (sup * sup < cpb) sup += 8;
+        }
+        std::vector<CRun> r1, r2, r3, r1b, r2b;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t g0 = (uint32_t)r1.size();
             for (uint32_t x = cfirst[b]; x < cfirst[b + 1]; x += sup) {
@@ -703,16 +737,28 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
                 r1.push_back(CRun{x, e, kIdentity, g});
                 r3.push_back(CRun{x, e, g, g});
             }
-            r2.push_back(CRun{g0, (uint32_t)r1.size(), kIdentity, 0});
+            const uint32_t g1 = (uint32_t)r1.size();
+            if (!s2) {
+                r2.push_back(CRun{g0, g1, kIdentity, 0});
+                continue;
+            }
+            const uint32_t h0 = (uint32_t)r1b.size();
+            for (uint32_t x = g0; x < g1; x += s2) {
+                const uint32_t h = (uint32_t)r1b.size(), e = std::min(g1, x + s2);
+                r1b.push_back(CRun{x, e, kIdentity, h});
+                r2b.push_back(CRun{x, e, h, 0});
+            }
+            r2.push_back(CRun{h0, (uint32_t)r1b.size(), kIdentity, 0});
         }
         nch = (uint32_t)hc.size();
         nhh = (uint32_t)hh.size();
         ng = (uint32_t)r1.size();
+        ng2 = (uint32_t)r1b.size();
         npk = pfirst[nb];
         // one staged upload: chunks | 64 K pieces | block offsets | pack-chunk firsts | runs
         const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
         const size_t tbo = (tb + 15) & ~(size_t)15;
-        const size_t tall = tbo + (2 * (size_t)ng + nb) * sizeof(CRun);
+        const size_t tall = tbo + (2 * (size_t)ng + nb + 2 * (size_t)ng2) * sizeof(CRun);
         std::vector<uint8_t> h(tall, 0);
         size_t o = 0;
         memcpy(&h[o], hc.data(), nch * sizeof(MChunk));
@@ -730,6 +776,12 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
         memcpy(&h[o], r3.data(), ng * sizeof(CRun));
         o += ng * sizeof(CRun);
         memcpy(&h[o], r2.data(), nb * sizeof(CRun));
+        o += nb * sizeof(CRun);
+        if (ng2) {
+            memcpy(&h[o], r1b.data(), ng2 * sizeof(CRun));
+            o += ng2 * sizeof(CRun);
+            memcpy(&h[o], r2b.data(), ng2 * sizeof(CRun));
+        }
         uint8_t *d_tab = (uint8_t *)c->get(WS_MTF_CHUNKS, tall + 64);
         c->h2d(d_tab, h.data(), tall);
         c->ws_tag[WS_MTF_CHUNKS] = sig;
@@ -737,6 +789,7 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
         c->ws_aux[WS_MTF_CHUNKS][1] = nhh;
         c->ws_aux[WS_MTF_CHUNKS][2] = ng;
         c->ws_aux[WS_MTF_CHUNKS][3] = npk;
+        c->ws_aux[WS_MTF_CHUNKS][4] = ng2;
     }
     const size_t tb = nch * sizeof(MChunk) + nhh * sizeof(HChunk) + 2 * (nb + 1) * 4;
     uint8_t *d_tab = (uint8_t *)c->ws[WS_MTF_CHUNKS];
@@ -745,22 +798,36 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint32_t *d_boffs = (uint32_t *)(d_tab + nch * sizeof(MChunk) + nhh * sizeof(HChunk));  // block offsets
     uint32_t *d_pfirst = d_boffs + (nb + 1);
     CRun *d_r1 = (CRun *)(d_tab + ((tb + 15) & ~(size_t)15)), *d_r3 = d_r1 + ng, *d_r2 = d_r3 + ng;
+    CRun *d_r1b = d_r2 + nb, *d_r2b = d_r1b + ng2;
     uint16_t *d_chist = (uint16_t *)c->get(WS_PACK_HIST, (size_t)npk * 256 * 2 + 64);
     uint8_t *d_R = (uint8_t *)c->get(WS_MTF_R, (size_t)nch * 256 + (size_t)nch * 4 + 64);
     uint32_t *d_dcount = (uint32_t *)(d_R + (size_t)nch * 256);
     uint32_t *d_S = (uint32_t *)c->get(WS_MTF_S, (size_t)nch * 256);
-    uint8_t *d_sup = (uint8_t *)c->get(WS_MTF_SUPER, (size_t)ng * (256 + 256 + 4) + 64);
+    // superchunk (then group) lists | start states | list lengths
+    uint8_t *d_sup = (uint8_t *)c->get(WS_MTF_SUPER, (size_t)(ng + ng2) * (256 + 256 + 4) + 64);
     uint8_t *d_Rg = d_sup;                                       // superchunk lists
     uint32_t *d_Sg = (uint32_t *)(d_sup + (size_t)ng * 256);     // superchunk start states
     uint32_t *d_dg = (uint32_t *)(d_sup + (size_t)ng * 512);     // superchunk list lengths
+    uint8_t *d_Rh = d_sup + (size_t)ng * 516;                    // group lists (five levels)
+    uint32_t *d_Sh = (uint32_t *)(d_Rh + (size_t)ng2 * 256);     // group start states
+    uint32_t *d_dh = (uint32_t *)(d_Rh + (size_t)ng2 * 512);     // group list lengths
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
     BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
     BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
                d_dg);
-    BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), nb, 64, 0, d_r2, d_Rg, d_dg, nullptr, d_Sg, nullptr,
-               nullptr);
+    if (ng2) {
+        BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng2, 64, 0, d_r1b, d_Rg, d_dg, nullptr, nullptr,
+                   d_Rh, d_dh);
+        BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), nb, 64, 0, d_r2, d_Rh, d_dh, nullptr, d_Sh,
+                   nullptr, nullptr);
+        BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng2, 64, 0, d_r2b, d_Rg, d_dg, d_Sh, d_Sg,
+                   nullptr, nullptr);
+    } else {
+        BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), nb, 64, 0, d_r2, d_Rg, d_dg, nullptr, d_Sg,
+                   nullptr, nullptr);
+    }
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng, 64, 0, d_r3, d_R, d_dcount, d_Sg, d_S, nullptr,
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);

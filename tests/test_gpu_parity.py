@@ -892,7 +892,7 @@ def test_compacted_alphabet_global_pass(ctx, oracle):
         assert recs[i] == oracle.encode(blocks[i]), (i, len(blocks[i]))
 
 
-def test_tuning_options_never_change_records(ctx):
+def test_tuning_options_never_change_records(ctx, oracle):
     """Every non-default bmh_ctx_set_option value (include/bmh.h BMH_OPT_*) once: pipelines 1..4
     and 5, MTF chunks 64 / 1024 / 4096, the list-round checker, and small stream / max batches on
     the host-buffer path, against the default encode of a mixed batch (random, Zipf text, a
@@ -903,6 +903,8 @@ def test_tuning_options_never_change_records(ctx):
     blocks += [z[i:i + (1 << 20)] for i in range(0, len(z), 1 << 20)]
     blocks += [bytes(200000) + b"\x01" * 100000, b"banana", b"a" * 40, rng.integers(0, 4, 70000, np.uint8).tobytes()]
     want = ctx.encode_blocks(blocks)
+    for i in (0, 6, 12, 15):  # the default's short MTF chunks take the five-level composition
+        assert want[i] == oracle.encode(blocks[i]), i
     try:
         for name, vals in (("pipelines", (1, 2, 3, 4, 5)), ("mtf_chunk", (64, 1024, 4096)), ("check_lists", (1,))):
             for v in vals:
@@ -949,3 +951,37 @@ def test_dense_probe_pipelines(ctx):
     ctx.encode_blocks_dev(d_in, offs, d_out, cap)
     assert ctx.last_pipelines() == 2
     ctx.set_option("pipelines", 0)
+
+
+def test_planted_ties_in_large_batch(ctx, oracle):
+    """Tied rotations in a 20 MiB batch (past the full-SA size, so the dense finish stores SA
+    only for segments a later pass reads): three config-4 random blocks (records equal the
+    reference manifest), a random block with planted ties — rotation 0's first 8 bytes copied to
+    three places (two in its own 16 K chunk), so rotation 0 sits in a tied group whose primary
+    the list pass sets; and a 3-byte pattern at 120 places, so one 12-bit sub-bucket holds > 64
+    rotations (a digit-level deferral) — and a random block of period 1000 (every rotation tied
+    far past 512 bits: the block needs rank doubling and the data phase re-runs with the full
+    suffix array). BWT of the crafted blocks equals the oracle's, and all records decode back.
+    (Written for the 6-byte record experiment of DESIGN §15, kept for the tie paths.)"""
+    bs = 4 << 20
+    rng = np.random.default_rng(77)
+    blocks = [synth.splitmix64_bytes(0, i * bs, bs).tobytes() for i in range(3)]
+    a = rng.integers(0, 256, bs, dtype=np.uint8)
+    for at in (1000, 5000, 3_000_000):
+        a[at:at + 8] = a[0:8]
+    pat = np.array([0x5A, 0xC3, 0x17], np.uint8)
+    for at in rng.choice(bs - 3, 120, replace=False):
+        a[at:at + 3] = pat
+    blocks.append(a.tobytes())
+    per = rng.integers(0, 256, 1000, dtype=np.uint8)
+    blocks.append(np.tile(per, bs // 1000 + 1)[:bs].tobytes())
+    recs = ctx.encode_blocks(blocks)
+    man = manifest("random_1g_4m")["blocks"]
+    for i in range(3):
+        assert hashlib.sha256(recs[i]).hexdigest() == man[i]["sha256"], i
+    for i in (3, 4):
+        prim, L = bmh.bwt(blocks[i], ctx)
+        oprim, oL = oracle.bwt(blocks[i])
+        assert prim == oprim and L == oL, i
+    for r, d in zip(recs, blocks):
+        assert ctx.decompress_bytes(r) == d
