@@ -192,7 +192,10 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
 {
     __shared__ uint32_t s_R[kComposeBatch][64];
     __shared__ uint32_t s_d[kComposeBatch];
-    __shared__ uint8_t s_S[256], s_flag[256];
+    // slots 256 + l: each lane's sink for masked-off stores (the step runs unbranched). One wave
+    // per workgroup: the steps' LDS hand-offs need only wave_sync (LDS executes a wave's
+    // operations in order; no wait for the stores before the loads that read them)
+    __shared__ uint8_t s_S[256 + 64], s_flag[256 + 64];
     const CRun run = runs[blockIdx.x];
     const uint32_t l = threadIdx.x, c0 = run.c0, c1 = run.c1;
     const uint32_t *R32 = (const uint32_t *)R;
@@ -212,6 +215,7 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
         pred = (l < kComposeBatch && cb + l < c1) ? dcount[cb + l] : 0u;
     };
     fetch(c0);
+    const uint32_t sink = 256 + l;
     for (uint32_t cb = c0; cb < c1; cb += kComposeBatch) {
         __syncthreads();
 #pragma unroll
@@ -220,15 +224,16 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
         __syncthreads();
         if (cb + kComposeBatch < c1) fetch(cb + kComposeBatch);
         const uint32_t ce = min(c1, cb + kComposeBatch);
+        uint32_t d = s_d[0], rw = s_R[0][l];  // this step's list; the next one is read with the state
         for (uint32_t c = cb; c < ce; ++c) {
             if (kSteps) Sout[(size_t)c * 64 + l] = st[0] | (st[1] << 8) | (st[2] << 16) | (st[3] << 24);
-            const uint32_t d = s_d[c - cb], rw = s_R[c - cb][l];
             *(uint32_t *)&s_flag[4 * l] = 0;
-            __syncthreads();
-            for (uint32_t k = 0; k < 4; ++k)
-                if (4 * l + k < d) s_flag[(rw >> (8 * k)) & 255u] = 1;
-            __syncthreads();
+            wave_sync();
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) s_flag[4 * l + k < d ? (rw >> (8 * k)) & 255u : sink] = 1;
+            wave_sync();
             uint32_t keep[4], cnt = 0, kt = 0;
+#pragma unroll
             for (int k = 0; k < 4; ++k) {
                 keep[k] = s_flag[st[k]] == 0;
                 cnt += keep[k];
@@ -236,13 +241,20 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
             }
             if (kFinal) dt = d + wave_sum_dpp(kt);
             uint32_t pos = d + wave_incl_sum_dpp(cnt) - cnt;
-            for (int k = 0; k < 4; ++k)
-                if (keep[k]) s_S[pos++] = (uint8_t)st[k];
-            for (uint32_t k = 0; k < 4; ++k)
-                if (4 * l + k < d) s_S[4 * l + k] = (uint8_t)(rw >> (8 * k));
-            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s_S[keep[k] ? pos : sink] = (uint8_t)st[k];
+                pos += keep[k];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) s_S[4 * l + k < d ? 4 * l + k : sink] = (uint8_t)(rw >> (8 * k));
+            wave_sync();
+            const uint32_t cn = c + 1 < ce ? c + 1 - cb : 0u;
+            d = s_d[cn];
+            rw = s_R[cn][l];
+#pragma unroll
             for (int k = 0; k < 4; ++k) st[k] = s_S[4 * l + k];
-            __syncthreads();
+            wave_sync();
         }
     }
     if (kFinal) {
