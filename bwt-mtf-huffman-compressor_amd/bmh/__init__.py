@@ -78,6 +78,7 @@ _SIGS = {
     "bmh_record_bound": (U64, [U64]),
     "bmh_encode_pipelines": (U32, [P, U64, U32]),
     "bmh_ctx_last_pipelines": (U32, [P]),
+    "bmh_ctx_spec_fallbacks": (U32, [P]),
     "bmh_compress_host": (C.c_int, [P, P, U64, U64, P, U64, PU64]),
     "bmh_compress_host_multi": (C.c_int, [C.POINTER(P), U32, P, U64, U64, P, U64, PU64]),
     "bmh_compress_bound": (U64, [U64, U64]),
@@ -247,6 +248,10 @@ class Context:
     def last_pipelines(self) -> int:
         """Pipelines the last encode_blocks_dev call ran on."""
         return int(lib().bmh_ctx_last_pipelines(self.h))
+
+    def spec_fallbacks(self) -> int:
+        """Batches re-encoded after their speculative list round left work (bmh.h)."""
+        return int(lib().bmh_ctx_spec_fallbacks(self.h))
 
     # ---- tuning options (include/bmh.h BMH_OPT_*; 0 restores the library's rule)
     OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5}

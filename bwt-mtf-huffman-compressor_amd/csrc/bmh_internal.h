@@ -100,8 +100,8 @@ struct Ctx {
     struct Options {
         uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0;
     } opt;
-    uint32_t last_pipelines = 0;
-    uint64_t zipf_resume_tok0 = 0, zipf_resume_base = 0;  // synth_zipf: start of its last round  // pipelines of the last device batch encode (encode_blocks)
+    uint32_t last_pipelines = 0;  // pipelines of the last device batch encode (encode_blocks)
+    uint64_t zipf_resume_tok0 = 0, zipf_resume_base = 0;  // synth_zipf: start of its last round
     uint64_t mtf_clen_sig = 0;  // MTF chunk length of the last batch layout (mtf.hip)
     uint32_t mtf_clen = 0;
     // size of the batch a sub-pipeline's sub-batch was cut from (0: its own batch): the run
@@ -111,6 +111,16 @@ struct Ctx {
     // BWT: write the suffix array of every slot (needed by rank doubling) instead of only the
     // slots later passes read; set after a batch needed doubling, cleared when one did not
     bool bwt_full_sa = false;
+    // speculative list round (bwt.hip): a dense batch on one pipeline runs its one expected
+    // (tiny) list round on a fixed grid without waiting for the list counters, and the MTF /
+    // Huffman / pack stages follow at once; encode_blocks_one reads the counters at its final
+    // sync (bwt_spec_ok) and encodes the batch again the waiting way if any list work was left
+    uint32_t *probe_host = nullptr, probe_cap = 0;  // dense_batch's census (pinned, written by the kernel)
+    hipEvent_t probe_ev = nullptr;
+    uint64_t pre_sig = 0;  // bwt_batch_core's prologue already launched for this input + layout
+    bool spec_lists = false, spec_pending = false;
+    uint32_t spec_fallbacks = 0;
+    uint32_t spec_cnt[128] = {};  // the list counters after the speculative round
     // host-buffer streaming (capi.cpp): copy streams and two pinned staging slots each way
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     static constexpr int kStageSlots = 3;  // host-buffer streaming: batches in flight (H2D / encode / D2H)
@@ -210,7 +220,11 @@ void bwt_batch(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint6
 Ctx *aux_ctx(Ctx *c);  // capi.cpp
 bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt);  // digram census (bwt_runs.hip)
 // the rotation sorter alone (bwt.hip); bwt_batch routes run-heavy blocks of small batches around it
-void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
+// prologue_only: launch the global pass's first kernels (up to the bucket scan) and return; the
+// next call for the same input and layout on this context skips them (Ctx::pre_sig)
+void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary,
+                    bool prologue_only = false);
+bool bwt_spec_ok(const Ctx *c);  // after the sync that follows a speculative list round
 void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint32_t *h_freq32,
                uint32_t *h_first32);
 void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_table *tables, uint8_t *d_out,

@@ -2306,13 +2306,33 @@ void build_tiles(const std::vector<S> &segs, uint32_t tile, std::vector<T> &tile
 
 }  // namespace
 
-void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary)
+constexpr uint32_t kSpecRows = 4;  // speculative tiny round: 4 * 4 * kTinyEpwShort = 256 entries per XCD lane
+
+bool bwt_spec_ok(const Ctx *c)
+{
+    const Counters *h = (const Counters *)c->spec_cnt;
+    if (h->lgroups || h->flagged) return false;
+    for (uint32_t x = 0; x < 8; ++x) {
+        if (h->lc[0][kListTiny][x] > kSpecRows * 4 * kTinyEpwShort) return false;
+        if (h->lc[0][kListFin][x] | h->lc[0][kListFinb][x] | h->lc[0][kListBig][x]) return false;
+        for (uint32_t cl = 0; cl < 4; ++cl)
+            if (h->lc[1][cl][x]) return false;
+    }
+    return true;
+}
+
+void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary,
+                    bool prologue_only)
 {
     const uint32_t nb = bt.nblocks;
     const uint64_t N = bt.total;
     const uint32_t big_cap = N > kBigCapLargeBatch ? kBigCapLarge : kBigCapSmall;
     if (N >= 0xffffffffull) fail(BMH_ERANGE, "bwt: batch must be < 4 GiB");
     WallPhase wall_data(c, "bwt_data");
+    // the prologue (k_phase_init .. k_g1_scan) may have been queued already (dense_batch)
+    const uint64_t psig = layout_sig(6, bt.offs, (uintptr_t)d_in);
+    bool pre_done = !prologue_only && c->pre_sig == psig;
+    c->pre_sig = 0;
 
     // ---- global-pass chunks, dealt into 8 XCD lanes (blocks b = lane mod 8); the table is
     // rebuilt and uploaded only when the batch layout changed since this context's last batch
@@ -2468,19 +2488,27 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         if (kb_cur != rec) std::swap(kb_cur, kb_nxt);  // the global pass writes its windows into rec
         static_assert(sizeof(Counters) % 4 == 0, "counter words");
         constexpr uint32_t kCntWords = sizeof(Counters) / 4;
-        BMH_LAUNCH(c, "bwt_fill", k_phase_init, cdiv(std::max(nb, kCntWords), 256), 256, 0, d_prim, bflag, nb,
-                   (uint32_t *)d_cnt, kCntWords);
+        if (!pre_done) {
+            BMH_LAUNCH(c, "bwt_fill", k_phase_init, cdiv(std::max(nb, kCntWords), 256), 256, 0, d_prim, bflag, nb,
+                       (uint32_t *)d_cnt, kCntWords);
 
-        // ---- data phase
-        // raw digits + each block's byte census, the blocks' alphabets, then the chunks of compacted
-        // blocks recounted
-        BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo, arank,
-                   abits, 0u);
-        BMH_LAUNCH(c, "bwt_g1_census", k_g1_census_fin, nb, 256, 0, abits, d_bchunks, d_bchunk0, ainfo, arank, rlist);
-        BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), 1024, 0, d_in, d_boffs, d_chunks,
-                   rlist, chist, ainfo, arank, abits, 1u);
-        BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0], lg[0],
-                   d_cnt, d_loff, big_cap, ainfo);
+            // ---- data phase
+            // raw digits + each block's byte census, the blocks' alphabets, then the chunks of
+            // compacted blocks recounted
+            BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo,
+                       arank, abits, 0u);
+            BMH_LAUNCH(c, "bwt_g1_census", k_g1_census_fin, nb, 256, 0, abits, d_bchunks, d_bchunk0, ainfo, arank,
+                       rlist);
+            BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), 1024, 0, d_in, d_boffs,
+                       d_chunks, rlist, chist, ainfo, arank, abits, 1u);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0],
+                       lg[0], d_cnt, d_loff, big_cap, ainfo);
+        }
+        pre_done = false;
+        if (prologue_only) {
+            c->pre_sig = psig;
+            return;
+        }
         set_out(0);
         BMH_LAUNCH(c, "bwt_g1_scatter", k_g1_scatter, nchunks, 1024, 0, da, d_chunks, chist, bk, rec);
         // the dense finish appends deferred segments after the global pass's list entries
@@ -2502,6 +2530,28 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             fprintf(stderr, "\n");
         }
 #endif
+        if (c->spec_lists && !full_sa && !dbg_lists && !h_primary) {
+            // speculative round (Ctx::spec_lists): on random-like data the global pass and the
+            // dense finish leave only a few tied pairs, all in the tiny list, which one round
+            // resolves. That round runs on a fixed grid (kSpecRows rows of 4 * kTinyEpwShort
+            // entries per XCD lane, identity lane map) without the host wait for the counters;
+            // the counters are read back at the encode's final sync and bwt_spec_ok checks that
+            // nothing was past the grid, in another list class, deferred again or sent to rank
+            // doubling. Saves two host round trips (≈ 70 µs of idle GPU on a 128 MiB batch).
+            set_out(1);  // (lc[1] zeroed by k_phase_init: the data phase appends to parity 0 only)
+            LaneMap lm;
+            for (uint32_t v = 0; v < 8; ++v) {
+                lm.lane[v] = (uint8_t)v;
+                lm.r[v] = 0;
+                lm.rep[v] = 1;
+            }
+            BMH_LAUNCH(c, "bwt_finish_tiny", k_finish_tiny, 8u * kSpecRows, 256, 0, da, lt[0], d_loff + kListTiny * 9,
+                       &d_cnt->lc[0][kListTiny][0], lm, kTinyEpwShort);
+            static_assert(sizeof(Counters) <= sizeof(c->spec_cnt), "spec counters");
+            c->d2h(c->spec_cnt, d_cnt, sizeof(Counters));
+            c->spec_pending = true;
+            return;
+        }
         // List rounds: every kernel of a round reads its list lengths from the device counters
         // and strides over them with a fixed grid, and the MSD tiles are built on the device, so
         // the host waits once per round (for the loop condition).
@@ -2565,7 +2615,8 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             }
             ++round;
             const uint32_t out = in ^ 1u;
-            BMH_HIP(hipMemsetAsync(&d_cnt->lc[out][0][0], 0, sizeof(d_cnt->lc[out]), c->stream));
+            // the parity this round appends to (round 1's is still zero from k_phase_init)
+            if (round > 1) BMH_HIP(hipMemsetAsync(&d_cnt->lc[out][0][0], 0, sizeof(d_cnt->lc[out]), c->stream));
             set_out(out);
             const uint32_t *dc = &d_cnt->lc[in][0][0];
             if (tot[kListTiny]) {

@@ -38,8 +38,6 @@
 
 namespace bmh {
 
-void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, uint64_t *h_primary);
-
 namespace {
 
 constexpr uint64_t kRunScreenMax = 64ull << 20;  // batches screened for run-heavy blocks
@@ -56,26 +54,28 @@ static_assert(kRunScreenMax / kRunShare <= kRunRankLimit, "a screened batch's ru
 // Digram census (dense_batch): distinct byte pairs among the first kProbeSample positions of each
 // block, one workgroup a block, a 65 536-bit LDS bitmap. Uniform-random bytes give ~14.5 K
 // distinct pairs in 16 K positions, text a few hundred to a few thousand.
-constexpr uint32_t kProbeSample = 16384;
-__global__ __launch_bounds__(256) void k_probe_digrams(const uint8_t *__restrict__ in, const uint64_t *__restrict__ boffs,
-                                                       uint32_t *__restrict__ out)
+constexpr uint32_t kProbeSample = 16384, kProbeNT = 1024;
+// boffs null: block b is [b * bs, b * bs + bs). out: pinned host memory (vector stores).
+__global__ __launch_bounds__(kProbeNT) void k_probe_digrams(const uint8_t *__restrict__ in,
+                                                            const uint64_t *__restrict__ boffs, uint64_t bs,
+                                                            uint32_t *__restrict__ out)
 {
     __shared__ uint32_t bm[2048];
     __shared__ uint32_t s_tot;
     const uint32_t b = blockIdx.x, t = threadIdx.x;
-    const uint64_t o = boffs[b];
-    const uint32_t m = (uint32_t)min<uint64_t>(boffs[b + 1] - o, kProbeSample);
-    for (uint32_t i = t; i < 2048; i += 256) bm[i] = 0;
+    const uint64_t o = boffs ? boffs[b] : b * bs;
+    const uint32_t m = (uint32_t)min<uint64_t>((boffs ? boffs[b + 1] : o + bs) - o, kProbeSample);
+    for (uint32_t i = t; i < 2048; i += kProbeNT) bm[i] = 0;
     if (t == 0) s_tot = 0;
     __syncthreads();
     const uint8_t *x = in + o;
-    for (uint32_t i = t; i + 1 < m; i += 256) {
+    for (uint32_t i = t; i + 1 < m; i += kProbeNT) {
         const uint32_t d = ((uint32_t)x[i] << 8) | x[i + 1];
         atomicOr(&bm[d >> 5], 1u << (d & 31u));
     }
     __syncthreads();
     uint32_t k = 0;
-    for (uint32_t i = t; i < 2048; i += 256) k += __builtin_popcount(bm[i]);
+    for (uint32_t i = t; i < 2048; i += kProbeNT) k += __builtin_popcount(bm[i]);
     k = wave_sum_dpp(k);
     if ((t & 63u) == 0) atomicAdd(&s_tot, k);
     __syncthreads();
@@ -624,24 +624,47 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
 // Whether a batch is dense (uniform-like bytes: the BWT's two data passes resolve it with one
 // short list round, no host-synchronised rounds), by the digram census of each block's first
 // 16 K positions: at least half of the sampled pairs distinct, for blocks holding >= 90 % of the
-// bytes. One launch and one host wait (~20-30 us). encode_blocks runs such batches on one
-// pipeline: on random data the pipelines only contend (128 MiB: 1.77 ms on one, 1.99 on four).
+// bytes. encode_blocks runs such batches on one pipeline: on random data the pipelines only
+// contend (128 MiB: 1.77 ms on one, 1.99 on four). One launch (1024 threads a block; block
+// offsets from the block size when the blocks are equal) whose counts land in pinned memory,
+// and one wait (≈ 60 -> ≈ 25 us of a 128 MiB batch's 1.7 ms: no staging copies).
 bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt)
 {
     const uint32_t nb = bt.nblocks;
+    const uint64_t bs = bt.offs[1];
+    bool uniform = true;
+    for (uint32_t b = 1; b < nb && uniform; ++b) uniform = bt.offs[b + 1] - bt.offs[b] == bs;
     uint8_t *d_misc = (uint8_t *)c->get(WS_RUN_MISC, (size_t)(nb + 1) * 8 + (size_t)nb * 8 + 1024);
     uint64_t *d_boffs = (uint64_t *)d_misc;
-    uint32_t *d_count = (uint32_t *)(d_misc + (size_t)(nb + 1) * 8);
-    std::vector<uint32_t> cnt(nb);
-    c->h2d(d_boffs, bt.offs.data(), (size_t)(nb + 1) * 8);
-    BMH_LAUNCH(c, "probe_digrams", k_probe_digrams, nb, 256, 0, d_in, d_boffs, d_count);
-    c->d2h(cnt.data(), d_count, (size_t)nb * 4);
-    c->sync();
+    if (c->probe_cap < nb) {
+        if (c->probe_host) {
+            BMH_HIP(hipStreamSynchronize(c->stream));
+            BMH_HIP(hipHostFree(c->probe_host));
+            c->probe_host = nullptr;
+        }
+        BMH_HIP(hipHostMalloc((void **)&c->probe_host, (size_t)nb * 4, hipHostMallocDefault));
+        c->probe_cap = nb;
+    }
+    if (!uniform) c->h2d(d_boffs, bt.offs.data(), (size_t)(nb + 1) * 8);
+    if (!c->probe_ev) BMH_HIP(hipEventCreateWithFlags(&c->probe_ev, hipEventDisableTiming));
+    BMH_LAUNCH(c, "probe_digrams", k_probe_digrams, nb, kProbeNT, 0, d_in, uniform ? nullptr : d_boffs, bs,
+               c->probe_host);
+    BMH_HIP(hipEventRecord(c->probe_ev, c->stream));
+    // a batch past the run screen that turns out dense runs bwt_batch_core on this context and
+    // stream: its global-pass prologue is queued behind the census now, so the GPU works through
+    // the host's wait and the launches that follow it (a batch kept on several pipelines leaves
+    // it unused: ~0.1 ms of one stream)
+    if (bt.total > kRunScreenMax && !c->opt.pipelines) bwt_batch_core(c, d_in, bt, nullptr, nullptr, true);
+    for (;;) {  // spin: a blocking wait can sleep the host thread for milliseconds
+        const hipError_t e = hipEventQuery(c->probe_ev);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) BMH_HIP(e);
+    }
     uint64_t dense = 0;
     for (uint32_t b = 0; b < nb; ++b) {
         const uint64_t n = bt.offs[b + 1] - bt.offs[b];
         const uint64_t m = std::min<uint64_t>(n, kProbeSample);
-        if (m >= 4096 && 2ull * cnt[b] >= m) dense += n;
+        if (m >= 4096 && 2ull * c->probe_host[b] >= m) dense += n;
     }
     return dense * 10 >= bt.total * 9;
 }

@@ -170,16 +170,25 @@ uint64_t record_bound(uint64_t n) { return kRecordHeader + 320 + n + 16; }
 
 // Device batch encode -> records at d_out; fills rec_offs (nblocks + 1).
 static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
-                              uint64_t *rec_offs, OffsetChain *chain, int sub)
+                              uint64_t *rec_offs, OffsetChain *chain, int sub, bool spec = false)
 {
     // BWT -> MTF (+ histograms) -> code books, record offsets and headers -> bit pack, all
     // on the context stream; the host waits on the BWT's list counters, and once at the end
+    // (spec: not even on the list counters, Ctx::spec_lists)
     const uint32_t nb = bt.nblocks;
     uint8_t *d_L = (uint8_t *)c->get(WS_L, bt.total);
     uint8_t *d_mtf = (uint8_t *)c->get(WS_MTF, bt.total);
     {
         WallPhase w(c, "bwt");
-        bwt_batch(c, d_in, bt, d_L, nullptr);
+        c->spec_lists = spec && !chain;
+        c->spec_pending = false;
+        try {
+            bwt_batch(c, d_in, bt, d_L, nullptr);
+        } catch (...) {
+            c->spec_lists = false;
+            throw;
+        }
+        c->spec_lists = false;
     }
     {
         WallPhase w(c, "mtf");
@@ -195,8 +204,14 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
     uint8_t *d_misc = (uint8_t *)c->get(WS_STATUS, (size_t)(nb + 1) * 8 + 64);
     uint32_t *d_status = (uint32_t *)d_misc;
     uint64_t *d_boffs = (uint64_t *)(d_misc + 64);
-    BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
-    c->h2d(d_boffs, bt.offs.data(), (nb + 1) * 8);
+    // status word zero and block offsets: set when the layout changes (get() clears the tag on
+    // reallocation), and the status word cleared again after an error is read below
+    const uint64_t sig = layout_sig(7, bt.offs, 0);
+    if (c->ws_tag[WS_STATUS] != sig) {
+        BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
+        c->h2d(d_boffs, bt.offs.data(), (nb + 1) * 8);
+        c->ws_tag[WS_STATUS] = sig;
+    }
     codebook_batch(c, bt, d_boffs, d_freq, d_first, d_prim, d_tabs, d_roffs, d_pay_offs, d_out, out_cap, d_status, chain,
                    sub);
     const uint16_t *d_chist = (const uint16_t *)c->get(WS_PACK_HIST, 64);  // written by mtf_batch
@@ -205,6 +220,18 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
     c->d2h(rec_offs, d_roffs, (nb + 1) * 8);
     c->d2h(&st, d_status, 4);
     c->sync();
+    if (st) {  // keep the status word zero for the next batch
+        BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
+        c->sync();
+    }
+    if (c->spec_pending) {
+        c->spec_pending = false;
+        if (!bwt_spec_ok(c)) {  // list work was left: the batch again, waiting on the counters
+            ++c->spec_fallbacks;
+            encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, chain, sub, false);
+            return;
+        }
+    }
     if (st & kStatusCapacity) fail(BMH_ERANGE, "encode: output capacity too small");
     if (st & kStatusEmpty) fail(BMH_EINVAL, "huffman: empty histogram (the reference segfaults on empty input)");
     if (st & kStatusCodeLen) fail(BMH_ERANGE, "huffman: code longer than 64 bits");
@@ -309,12 +336,17 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
     // pipelines only contend (128 / 256 MiB of 4 MiB blocks: 1.99 / 3.49 ms against 1.77 / 3.14
     // on one; 1 GiB: equal), while text keeps them for its host-synchronised list rounds
     // (Zipf 128 MB at 4 MiB blocks: 14.1 ms on four, 16.8 on one)
+    // (and, on one pipeline, run their one expected list round speculatively: Ctx::spec_lists)
+    bool spec = false;
     if (S > 1 && !c->opt.pipelines && bt.total >= kDenseProbeMin && bt.total <= kDenseProbeMax &&
-        dense_batch(c, d_in, bt))
+        dense_batch(c, d_in, bt)) {
         S = 1;
+        spec = true;
+    }
+    c->pre_sig = spec ? c->pre_sig : 0;  // a prologue dense_batch launched for one pipeline, unused
     c->last_pipelines = (uint32_t)std::max(S, 1);
     if (S <= 1) {
-        encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0);
+        encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0, spec);
         return;
     }
     std::vector<uint32_t> cut(S + 1, nb);
@@ -822,9 +854,11 @@ void bmh_ctx_destroy(bmh_ctx *c)
     c->subs.clear();
     if (c->aux) bmh_ctx_destroy(static_cast<bmh_ctx *>(c->aux));
     c->aux = nullptr;
-    if (c->arena) (void)hipHostFree(c->arena);
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->arena) (void)hipHostFree(c->arena);
+    if (c->probe_host) (void)hipHostFree(c->probe_host);
+    if (c->probe_ev) (void)hipEventDestroy(c->probe_ev);
     for (int s = 0; s < WS_COUNT_; ++s)
         if (c->ws[s]) (void)hipFree(c->ws[s]);
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -985,6 +1019,7 @@ uint32_t bmh_encode_pipelines(bmh_ctx *c, uint64_t total, uint32_t nblocks)
 }
 
 uint32_t bmh_ctx_last_pipelines(bmh_ctx *c) { return c ? c->last_pipelines : 0u; }
+uint32_t bmh_ctx_spec_fallbacks(bmh_ctx *c) { return c ? c->spec_fallbacks : 0u; }
 
 uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
 {

@@ -989,6 +989,7 @@ void decode_blocks(Ctx *c, const uint8_t *d_rec, const uint64_t *rec_offs, uint3
     c->h2d(d_ch_block, ch_block.data(), nch * 4);
     c->h2d(d_ich, ich.data(), nch * sizeof(IChunk));
     uint32_t *d_status = (uint32_t *)c->get(WS_STATUS, 256);
+    c->ws_tag[WS_STATUS] = 0;  // the encode's status word / block offsets (capi.cpp) are rewritten
     BMH_HIP(hipMemsetAsync(d_status, 0, 16, c->stream));
 
     // ---- Huffman^-1 -> d_mtf (batch layout = output layout)

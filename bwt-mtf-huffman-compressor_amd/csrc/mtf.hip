@@ -91,12 +91,15 @@ struct MChunk {
 // atomicMax of positions, a bitset of last-occurrence positions (lane l owns the 64 positions
 // from 64l), then each symbol's rank = set bits above its last position (wave scan + one
 // popcount), and the symbol is stored at its rank.
+// (also zeroes the block histograms k_mtf_hist accumulates: no memset launch)
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
-                                                     uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount)
+                                                     uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount,
+                                                     uint32_t *__restrict__ freq, uint32_t nfreq)
 {
     __shared__ int lastpos[4][256];
     __shared__ uint32_t bset[4][kMtfChunk / 32];
     __shared__ uint32_t above[4][64];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nfreq; i += gridDim.x * 256) freq[i] = 0;
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u, c = blockIdx.x * 4 + w;
     if (c >= nch) return;  // the whole wave
     const MChunk ch = chunks[c];
@@ -825,8 +828,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint32_t *d_dh = (uint32_t *)(d_Rh + (size_t)ng2 * 512);     // group list lengths
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
-    BMH_HIP(hipMemsetAsync(d_freq, 0, (size_t)nb * 256 * 4, c->stream));
-    BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount);
+    BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount, d_freq,
+               nb * 256);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
                d_dg);
     if (ng2) {

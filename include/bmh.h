@@ -131,6 +131,10 @@ uint32_t bmh_encode_pipelines(bmh_ctx *ctx, uint64_t total, uint32_t nblocks);
 /* Pipelines the context's last bmh_encode_blocks_dev call ran on: the rule above, or 1 when a
  * 32-256 MiB batch's digram census found it dense (uniform-like bytes). */
 uint32_t bmh_ctx_last_pipelines(bmh_ctx *ctx);
+/* Dense one-pipeline batches run their one expected BWT list round without waiting for its
+ * counts and check them at the end; this counts the context's batches whose check found list
+ * work left, so they were encoded again the waiting way (records are the same either way). */
+uint32_t bmh_ctx_spec_fallbacks(bmh_ctx *ctx);
 /* Capacity sufficient for one record of an n-byte block. */
 uint64_t bmh_record_bound(uint64_t n);
 

@@ -953,6 +953,46 @@ def test_dense_probe_pipelines(ctx):
     ctx.set_option("pipelines", 0)
 
 
+def test_speculative_list_round_fallback(ctx, oracle):
+    """Dense one-pipeline batches run their tiny list round without the host wait and check its
+    counters at the end (bwt.hip bwt_spec_ok): a 48 MiB random batch needs no fallback (records
+    = the config-4 manifest's); the same batch with a 2 KB stretch of block 5 repeated inside the
+    block (rotations tied for up to 16 K bits: more list rounds, then rank doubling) falls back
+    once and its records equal the reference's; then a clean batch speculates again."""
+    bs, nblk = 4 << 20, 12
+    offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
+    d_in = ctx.alloc(bs * nblk)
+    for i in range(nblk):
+        ctx.synth_splitmix64(d_in.ptr.value + i * bs, bs, 0, i * bs)
+    cap = nblk * int(bmh.lib().bmh_record_bound(bs))
+    d_out = ctx.alloc(cap)
+    man = manifest("random_1g_4m")["blocks"]
+
+    def run():
+        ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+        assert ctx.last_pipelines() == 1
+        recs = d_out.download(int(ro[-1])).tobytes()
+        return [recs[int(ro[b]):int(ro[b + 1])] for b in range(nblk)]
+
+    f0 = ctx.spec_fallbacks()
+    recs = run()
+    assert ctx.spec_fallbacks() == f0
+    for b in range(nblk):
+        assert hashlib.sha256(recs[b]).hexdigest() == man[b]["sha256"], b
+    blk = bytearray(synth.splitmix64_bytes(0, 5 * bs, bs).tobytes())
+    blk[2_000_000:2_002_048] = blk[1000:3048]
+    d_in.upload(np.frombuffer(bytes(blk), np.uint8), offset=5 * bs)
+    recs = run()
+    assert ctx.spec_fallbacks() == f0 + 1
+    assert recs[5] == oracle.encode(bytes(blk))
+    for b in (0, 4, 6, 11):
+        assert hashlib.sha256(recs[b]).hexdigest() == man[b]["sha256"], b
+    ctx.synth_splitmix64(d_in.ptr.value + 5 * bs, bs, 0, 5 * bs)
+    recs = run()
+    assert ctx.spec_fallbacks() == f0 + 1
+    assert hashlib.sha256(recs[5]).hexdigest() == man[5]["sha256"]
+
+
 def test_planted_ties_in_large_batch(ctx, oracle):
     """Tied rotations in a 20 MiB batch (past the full-SA size, so the dense finish stores SA
     only for segments a later pass reads): three config-4 random blocks (records equal the
