@@ -157,9 +157,14 @@ __device__ __forceinline__ uint32_t head_bits16(const uint8_t *__restrict__ t, u
     return f;
 }
 // One workgroup: exclusive prefix (op = sum, or max with identity 0) of cnt[0..m) into out.
+// gate (doubling rounds, k_round_gate): non-null and set -> the round is past its last, no work
+#define RUN_GATED(gate) \
+    if ((gate) && *(gate)) return
 template <bool MAX>
-__global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict__ cnt, uint32_t m, uint32_t *__restrict__ out)
+__global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict__ cnt, uint32_t m, uint32_t *__restrict__ out,
+                                                     const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t s_tmp[17];
     const uint32_t per = (m + 1023) / 1024, t = threadIdx.x, a = min(m, t * per), e = min(m, a + per);
     uint32_t acc = 0;
@@ -183,8 +188,9 @@ __global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict_
 constexpr uint32_t kRsBits = 11, kRsBins = 1u << kRsBits, kRsDPT = kRsBins / 256;  // digits per thread
 constexpr uint32_t kRsTile = 4096, kRsInlineTiles = 16;  // inline: each tile reads kRsBins x tiles counts
 __global__ __launch_bounds__(256) void k_rsort_hist(const uint64_t *__restrict__ key, uint32_t n, uint32_t shift,
-                                                    uint32_t ntiles, uint32_t *__restrict__ cnt)
+                                                    uint32_t ntiles, uint32_t *__restrict__ cnt, const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t h[kRsBins];
     const uint32_t t = threadIdx.x;
     for (uint32_t d = t; d < kRsBins; d += 256) h[d] = 0;
@@ -198,8 +204,10 @@ __global__ __launch_bounds__(256) void k_rsort_hist(const uint64_t *__restrict__
     for (uint32_t d = t; d < kRsBins; d += 256) cnt[(size_t)d * ntiles + blockIdx.x] = h[d];
 }
 // grid = kRsBins digits: row d of cnt -> exclusive prefix over the tiles (in place), total in dtot[d]
-__global__ __launch_bounds__(256) void k_rsort_rows(uint32_t *__restrict__ cnt, uint32_t ntiles, uint32_t *__restrict__ dtot)
+__global__ __launch_bounds__(256) void k_rsort_rows(uint32_t *__restrict__ cnt, uint32_t ntiles, uint32_t *__restrict__ dtot,
+                                                    const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t s_tmp[8];
     uint32_t *row = cnt + (size_t)blockIdx.x * ntiles;
     uint32_t carry = 0;
@@ -219,8 +227,9 @@ template <bool INLINE>
 __global__ __launch_bounds__(256) void k_rsort_scatter(const uint64_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                        uint64_t *__restrict__ kout, uint32_t *__restrict__ vout, uint32_t n,
                                                        uint32_t shift, uint32_t ntiles, const uint32_t *__restrict__ cnt,
-                                                       const uint32_t *__restrict__ dtot)
+                                                       const uint32_t *__restrict__ dtot, const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t s_wc[4][kRsBins + 1], s_tmp[8];
     const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
     // thread t owns digits kRsDPT t .. kRsDPT t + kRsDPT - 1: their totals and this tile's prefix
@@ -315,8 +324,9 @@ __global__ __launch_bounds__(256) void k_rsort_copy(const uint64_t *__restrict__
 // first sorted slot of each key's group (0 elsewhere) per thread run of 16 slots, the tile's
 // largest (its last head) in tmax, and the group count
 __global__ __launch_bounds__(256) void k_group_heads(const uint64_t *__restrict__ sk, uint32_t m, uint32_t *__restrict__ tmax,
-                                                     uint32_t *__restrict__ ngroups)
+                                                     uint32_t *__restrict__ ngroups, const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t s_tmp[8];
     const uint32_t j0 = blockIdx.x * kPrimTile + 16u * threadIdx.x;
     uint32_t last = 0, heads = 0;
@@ -337,8 +347,9 @@ __global__ __launch_bounds__(256) void k_group_heads(const uint64_t *__restrict_
 // then within the tile a workgroup max-scan over the 16-slot runs
 __global__ __launch_bounds__(256) void k_rank_scatter(const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sidx,
                                                       uint32_t m, const uint32_t *__restrict__ tpre,
-                                                      uint32_t *__restrict__ rank)
+                                                      uint32_t *__restrict__ rank, const uint32_t *gate)
 {
+    RUN_GATED(gate);
     __shared__ uint32_t s_tmp[8];
     const uint32_t j0 = blockIdx.x * kPrimTile + 16u * threadIdx.x, e = min(m, j0 + 16u);
     uint32_t last = 0;
@@ -411,11 +422,23 @@ __global__ __launch_bounds__(256) void k_brun_keys(const uint8_t *__restrict__ i
     idx[i] = i;
 }
 
+// Start of a doubling round: cnt[0] = the previous round's group count. All groups distinct ->
+// cnt[1] (the gate) set and the round's kernels return at once; else the count restarts.
+__global__ void k_round_gate(uint32_t *cnt, uint32_t M)
+{
+    if (threadIdx.x == 0) {
+        const uint32_t stop = cnt[0] >= M;
+        cnt[1] = stop;
+        if (!stop) cnt[0] = 0;
+    }
+}
+
 // (rank_i, rank of the run h further on in the same block, cyclic) packed in 2 * bits, value i
 __global__ __launch_bounds__(256) void k_bpair_keys(const RBlk *__restrict__ tab, const uint32_t *__restrict__ rblk,
                                                     const uint32_t *__restrict__ rank, uint32_t M, uint32_t h, uint32_t bits,
-                                                    uint64_t *__restrict__ key, uint32_t *__restrict__ idx)
+                                                    uint64_t *__restrict__ key, uint32_t *__restrict__ idx, const uint32_t *gate)
 {
+    RUN_GATED(gate);
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
     if (i >= M) return;
     const RBlk B = tab[rblk[i]];
@@ -532,42 +555,50 @@ RunWs run_ws(Ctx *c, uint64_t N, uint32_t M, uint32_t NT, uint32_t B)
 }
 
 // Ranks of sorted keys sk (m of them, values sidx): rank[sidx[j]] = first slot of sk[j]'s
-// group. Returns the group count (one host wait).
-uint32_t rank_groups(Ctx *c, RunWs &w, const uint64_t *sk, const uint32_t *sidx, uint32_t m, uint32_t *h_cnt)
+// group; the group count lands in w.cnt[0] (zeroed before: by a memset, or by k_round_gate).
+void rank_groups_async(Ctx *c, RunWs &w, const uint64_t *sk, const uint32_t *sidx, uint32_t m, const uint32_t *gate)
 {
     const uint32_t nt = cdiv(m, kPrimTile);
+    BMH_LAUNCH(c, "bwt_run_groups", k_group_heads, nt, 256, 0, sk, m, w.tcnt, w.cnt, gate);
+    BMH_LAUNCH(c, "bwt_run_scan", k_tiles_excl<true>, 1, 1024, 0, w.tcnt, nt, w.toff, gate);
+    BMH_LAUNCH(c, "bwt_run_groups", k_rank_scatter, nt, 256, 0, sk, sidx, m, w.toff, w.rank, gate);
+}
+// The same, returning the group count (one host wait).
+uint32_t rank_groups(Ctx *c, RunWs &w, const uint64_t *sk, const uint32_t *sidx, uint32_t m, uint32_t *h_cnt)
+{
     BMH_HIP(hipMemsetAsync(w.cnt, 0, 4, c->stream));
-    BMH_LAUNCH(c, "bwt_run_groups", k_group_heads, nt, 256, 0, sk, m, w.tcnt, w.cnt);
-    BMH_LAUNCH(c, "bwt_run_scan", k_tiles_excl<true>, 1, 1024, 0, w.tcnt, nt, w.toff);
-    BMH_LAUNCH(c, "bwt_run_groups", k_rank_scatter, nt, 256, 0, sk, sidx, m, w.toff, w.rank);
+    rank_groups_async(c, w, sk, sidx, m, nullptr);
     c->d2h(h_cnt, w.cnt, 4);
     c->sync();
     return *h_cnt;
 }
 
-// Stable sort of cnt (key, value) pairs by key bits [0, end_bit): result in (kout, vout); kin /
-// vin are scratch (overwritten).
-void sort_pairs(Ctx *c, RunWs &w, uint64_t *kin, uint64_t *kout, uint32_t *vin, uint32_t *vout, uint32_t cnt,
-                uint32_t end_bit)
+// Stable sort of cnt (key, value) pairs by key bits [0, end_bit): result in (kout, vout), or
+// (any_out) in whichever of the two buffers the last pass wrote (returned: true = kin / vin);
+// the other pair is scratch.
+bool sort_pairs(Ctx *c, RunWs &w, uint64_t *kin, uint64_t *kout, uint32_t *vin, uint32_t *vout, uint32_t cnt,
+                uint32_t end_bit, const uint32_t *gate = nullptr, bool any_out = false)
 {
     const uint32_t nt = cdiv(cnt, kRsTile), passes = (end_bit + kRsBits - 1) / kRsBits;
     uint64_t *ks = kin, *kd = kout;
     uint32_t *vs = vin, *vd = vout;
     for (uint32_t ps = 0; ps < passes; ++ps) {
         const uint32_t sh = kRsBits * ps;
-        BMH_LAUNCH(c, "bwt_run_sort", k_rsort_hist, nt, 256, 0, ks, cnt, sh, nt, w.rowpre);
+        BMH_LAUNCH(c, "bwt_run_sort", k_rsort_hist, nt, 256, 0, ks, cnt, sh, nt, w.rowpre, gate);
         if (nt <= kRsInlineTiles) {
             BMH_LAUNCH(c, "bwt_run_sort", k_rsort_scatter<true>, nt, 256, 0, ks, vs, kd, vd, cnt, sh, nt, w.rowpre,
-                       w.dtot);
+                       w.dtot, gate);
         } else {
-            BMH_LAUNCH(c, "bwt_run_sort", k_rsort_rows, kRsBins, 256, 0, w.rowpre, nt, w.dtot);
+            BMH_LAUNCH(c, "bwt_run_sort", k_rsort_rows, kRsBins, 256, 0, w.rowpre, nt, w.dtot, gate);
             BMH_LAUNCH(c, "bwt_run_sort", k_rsort_scatter<false>, nt, 256, 0, ks, vs, kd, vd, cnt, sh, nt, w.rowpre,
-                       w.dtot);
+                       w.dtot, gate);
         }
         std::swap(ks, kd);
         std::swap(vs, vd);
     }
+    if (any_out) return ks == kin;
     if (ks != kout) BMH_LAUNCH(c, "bwt_run_sort", k_rsort_copy, cdiv(cnt, 256), 256, 0, ks, vs, kout, vout, cnt);
+    return false;
 }
 
 // The BWT of run-heavy blocks, all at once: block i = bytes [offs[i], offs[i] + ns[i]) of the
@@ -601,17 +632,44 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
         const dim3 tgrid(cdiv(maxn, kPrimTile), B);
         BMH_HIP(hipMemsetAsync(w.tcnt, 0, (size_t)NT * 4, c->stream));
         BMH_LAUNCH(c, "bwt_run_heads", k_bheads_count, tgrid, 256, 0, in, w.tab, w.tcnt);
-        BMH_LAUNCH(c, "bwt_run_heads", k_tiles_excl<false>, 1, 1024, 0, w.tcnt, NT, w.toff);
+        BMH_LAUNCH(c, "bwt_run_heads", k_tiles_excl<false>, 1, 1024, 0, w.tcnt, NT, w.toff, nullptr);
         BMH_LAUNCH(c, "bwt_run_heads", k_bheads_write, tgrid, 256, 0, in, w.tab, w.toff, w.H, w.rblk);
         BMH_LAUNCH(c, "bwt_run_keys", k_brun_keys, cdiv(M, 256), 256, 0, in, w.tab, w.H, w.rblk, M, w.key, w.idx);
         sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 33 + bb);
-        uint32_t groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
+        const uint32_t groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
         const uint32_t bits = bits_for(M - 1);
-        for (uint64_t h = 1; groups < M && h < maxm; h *= 2) {
-            BMH_LAUNCH(c, "bwt_run_keys", k_bpair_keys, cdiv(M, 256), 256, 0, w.tab, w.rblk, w.rank, M, (uint32_t)h, bits,
-                       w.key, w.idx);
-            sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 2 * bits);
-            groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
+        // prefix doubling over the run sequence: round h sorts (rank_i, rank_{i+h}) and re-ranks,
+        // until all ranks differ (or h >= the longest run sequence). The host reads each round's
+        // group count one round late: round h + 1 is queued before the wait for round h's count,
+        // gated on the device by that count (k_round_gate), so the GPU never idles on the wait;
+        // the one round queued past the last costs its empty launches.
+        if (groups < M && maxm > 1) {
+            if (!c->run_cnt_host) BMH_HIP(hipHostMalloc((void **)&c->run_cnt_host, 64, hipHostMallocDefault));
+            for (auto &e : c->run_ev)
+                if (!e) BMH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            const uint32_t *gate = w.cnt + 1;
+            auto launch_round = [&](uint64_t h, int slot) {
+                BMH_LAUNCH(c, "bwt_run_groups", k_round_gate, 1, 64, 0, w.cnt, M);
+                BMH_LAUNCH(c, "bwt_run_keys", k_bpair_keys, cdiv(M, 256), 256, 0, w.tab, w.rblk, w.rank, M, (uint32_t)h,
+                           bits, w.key, w.idx, gate);
+                const bool in_key = sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 2 * bits, gate, true);
+                rank_groups_async(c, w, in_key ? w.key : w.key2, in_key ? w.idx : w.idx2, M, gate);
+                BMH_HIP(hipMemcpyAsync(c->run_cnt_host + slot, w.cnt, 4, hipMemcpyDeviceToHost, c->stream));
+                BMH_HIP(hipEventRecord(c->run_ev[slot], c->stream));
+            };
+            uint64_t h = 1;
+            launch_round(h, 0);
+            for (int r = 0;; ++r) {
+                const bool more = 2 * h < maxm;
+                if (more) launch_round(2 * h, (r + 1) & 1);
+                for (;;) {  // spin: a blocking wait can sleep the host thread for milliseconds
+                    const hipError_t e = hipEventQuery(c->run_ev[r & 1]);
+                    if (e == hipSuccess) break;
+                    if (e != hipErrorNotReady) BMH_HIP(e);
+                }
+                if (c->run_cnt_host[r & 1] >= M || !more) break;  // a queued round past this is gated
+                h *= 2;
+            }
         }
         const dim3 pgrid(cdiv(maxn, 256), B);
         BMH_LAUNCH(c, "bwt_run_place", k_bpos_keys, pgrid, 256, 0, in, w.tab, w.H, w.rank, w.pkey, w.pval);
