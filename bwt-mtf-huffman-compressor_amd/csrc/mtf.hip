@@ -91,15 +91,20 @@ struct MChunk {
 // atomicMax of positions, a bitset of last-occurrence positions (lane l owns the 64 positions
 // from 64l), then each symbol's rank = set bits above its last position (wave scan + one
 // popcount), and the symbol is stored at its rank.
-// (also zeroes the block histograms k_mtf_hist accumulates: no memset launch)
+// (also resets what k_mtf_hist accumulates: the block histograms and first pack chunks; no
+// memset launches)
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                      uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount,
-                                                     uint32_t *__restrict__ freq, uint32_t nfreq)
+                                                     uint32_t *__restrict__ freq, uint32_t *__restrict__ firstc,
+                                                     uint32_t nfreq)
 {
     __shared__ int lastpos[4][256];
     __shared__ uint32_t bset[4][kMtfChunk / 32];
     __shared__ uint32_t above[4][64];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nfreq; i += gridDim.x * 256) freq[i] = 0;
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nfreq; i += gridDim.x * 256) {
+        freq[i] = 0;
+        firstc[i] = 0xffffffffu;
+    }
     const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u, c = blockIdx.x * 4 + w;
     if (c >= nch) return;  // the whole wave
     const MChunk ch = chunks[c];
@@ -134,9 +139,14 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
         }
     }
     wave_sync();
+    // a symbol followed by itself in the lane's span is not its last occurrence there: one atomic
+    // per run of equal symbols (a text block's last column is mostly runs)
 #pragma unroll
-    for (uint32_t k = 0; k < 64; ++k)
-        if (k < nv) atomicMax(&lastpos[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], (int)(e0 + k));
+    for (uint32_t k = 0; k < 64; ++k) {
+        const uint32_t x = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
+        const bool again = k + 1 < 64 && k + 1 < nv && ((sw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 255u) == x;
+        if (k < nv && !again) atomicMax(&lastpos[w][x], (int)(e0 + k));
+    }
     wave_sync();
     uint32_t d = 0;
     int lp[4];
@@ -532,10 +542,11 @@ struct HChunk {
 // 4 K-symbol pack chunk (u16; the pack sizes its chunks from these instead of re-reading the
 // MTF stream). One workgroup per 64 K symbols of a block; wave w takes pack chunk w (lane l:
 // symbols [64l, 64l + 64), one 64-byte sector) with its own LDS histogram, no workgroup
-// barrier until the block totals. First occurrences come from k_mtf_first.
+// barrier until the block totals. firstc[b][v] = the first pack chunk holding v (atomicMin over
+// the workgroups); the first occurrences inside those chunks come from k_mtf_first.
 __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
                                                    const uint32_t *__restrict__ pfirst, uint32_t *__restrict__ freq,
-                                                   uint16_t *__restrict__ chist)
+                                                   uint16_t *__restrict__ chist, uint32_t *__restrict__ firstc)
 {
     constexpr uint32_t NW = 65536 / kPackChunkSyms;
     __shared__ uint32_t h[NW][256];
@@ -558,10 +569,20 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
                 sw[4 * q + 2] = v.z;
                 sw[4 * q + 3] = v.w;
             }
+            // values 0 and 1 (most of a text block's MTF output) counted in a register: LDS
+            // atomics on one address from many lanes serialise
+            uint32_t z01 = 0;
 #pragma unroll
             for (uint32_t k = 0; k < 64; ++k) {
                 const uint32_t v = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
-                atomicAdd(&h[w][v], 1u);
+                z01 += v < 2 ? 1u << (16 * v) : 0u;
+                if (v >= 2) atomicAdd(&h[w][v], 1u);
+            }
+            z01 = wave_sum_dpp(z01);  // <= 4096 per value: two 16-bit fields
+            wave_sync();
+            if (l == 0) {
+                h[w][0] += z01 & 0xffffu;
+                h[w][1] += z01 >> 16;
             }
         } else {
             for (uint32_t k = 0; k < 64 && e0 + k < len; ++k) atomicAdd(&h[w][in[a + e0 + k]], 1u);
@@ -573,16 +594,21 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
     }
     __syncthreads();
     if (t < 256) {
-        uint32_t tot = 0;
+        uint32_t tot = 0, fx = NW;
 #pragma unroll
-        for (uint32_t x = 0; x < NW; ++x) tot += h[x][t];
-        if (tot) atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
+        for (uint32_t x = 0; x < NW; ++x) {
+            tot += h[x][t];
+            fx = fx == NW && h[x][t] ? x : fx;
+        }
+        if (tot) {
+            atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
+            atomicMin(&firstc[(size_t)ch.block * 256 + t], ch.rel / kPackChunkSyms + fx);
+        }
     }
 }
 
 // First occurrence of each MTF value per block (huffman() main.cpp:238-244 orders the leaves
-// by it). The pack-chunk histograms say in which chunk each value first appears (value v:
-// the first chunk with a nonzero count, found 16 chunks per step); only those chunks are
+// by it). k_mtf_hist found the chunk each value first appears in (firstc); only those chunks are
 // scanned (on random data: the block's first chunk alone), one wave per distinct chunk. A value
 // has one first chunk, so the chunks are independent and need no order. Grid (blocks,
 // kFirstWG): every workgroup of a block derives the same sorted list of distinct first chunks
@@ -593,7 +619,7 @@ constexpr uint32_t kFirstNT = 1024, kFirstWG = 8, kFirstBmWords = 256;  // bitma
 __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restrict__ in, const uint32_t *__restrict__ boffs,
                                                         const uint32_t *__restrict__ pfirst,
                                                         const uint32_t *__restrict__ freq,
-                                                        const uint16_t *__restrict__ chist, uint32_t *__restrict__ first)
+                                                        const uint32_t *__restrict__ firstc, uint32_t *__restrict__ first)
 {
     __shared__ uint32_t f[256], s_cv[256], s_list[256], s_nlist, s_bm[kFirstBmWords], s_tmp[kFirstNT / 64 + 1];
     const uint32_t b = blockIdx.x, g = blockIdx.y, t = threadIdx.x, w = t >> 6, l = t & 63u;
@@ -605,30 +631,9 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
     if (t < kFirstBmWords) s_bm[t] = 0;
     if (t < 256) {
         f[t] = 0xffffffffu;
-        s_cv[t] = 0xffffffffu;  // first chunk holding t (block-relative); none for absent values
+        // first chunk holding t (block-relative); none for absent values
+        s_cv[t] = freq[(size_t)b * 256 + t] ? firstc[(size_t)b * 256 + t] : 0xffffffffu;
     }
-    __syncthreads();
-    {
-        // value v = t & 255 searched by 4 threads, thread q over the chunk groups 16 q + 64 i:
-        // a value first seen late in a long block (Calgary's text files: ~200 chunks) costs a
-        // quarter of the dependent load rounds; each thread stops at its first hit
-        const uint32_t v = t & 255u, q = t >> 8;
-        bool look = freq[(size_t)b * 256 + v] != 0;
-        for (uint32_t base = 16 * q; look && base < nc; base += 64) {
-            uint32_t cnt[16];
-#pragma unroll
-            for (uint32_t j = 0; j < 16; ++j) cnt[j] = base + j < nc ? chist[(size_t)(c0 + base + j) * 256 + v] : 0u;
-            uint32_t cv = 0xffffffffu;
-#pragma unroll
-            for (int j = 15; j >= 0; --j)
-                if (cnt[j]) cv = base + j;
-            if (cv != 0xffffffffu) {
-                atomicMin(&s_cv[v], cv);
-                look = false;
-            }
-        }
-    }
-    static_assert(kFirstNT == 1024, "k_mtf_first: four searching threads per value");
     __syncthreads();
     if (bitmap) {
         if (t < 256 && s_cv[t] != 0xffffffffu) atomicOr(&s_bm[s_cv[t] >> 5], 1u << (s_cv[t] & 31u));
@@ -677,9 +682,10 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
         }
         const uint32_t m = e0 < len ? min(64u, len - e0) : 0u;
 #pragma unroll
-        for (uint32_t j = 0; j < 64; ++j) {
+        for (uint32_t j = 0; j < 64; ++j) {  // (a value repeating the one before is not a first one)
             const uint32_t x = (sw[j >> 2] >> (8 * (j & 3))) & 255u;
-            if (j < m && s_cv[x] == cm) atomicMin(&f[x], p0 + e0 + j);
+            const bool again = j > 0 && ((sw[(j - 1) >> 2] >> (8 * ((j - 1) & 3))) & 255u) == x;
+            if (j < m && !again && s_cv[x] == cm) atomicMin(&f[x], p0 + e0 + j);
         }
     }
     __syncthreads();
@@ -827,9 +833,10 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint32_t *d_Sh = (uint32_t *)(d_Rh + (size_t)ng2 * 256);     // group start states
     uint32_t *d_dh = (uint32_t *)(d_Rh + (size_t)ng2 * 512);     // group list lengths
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
-    uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
+    uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 8);
+    uint32_t *d_firstc = d_first + (size_t)nb * 256;  // first pack chunk of each value (k_mtf_hist)
     BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount, d_freq,
-               nb * 256);
+               d_firstc, nb * 256);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
                d_dg);
     if (ng2) {
@@ -846,8 +853,8 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng, 64, 0, d_r3, d_R, d_dcount, d_Sg, d_S, nullptr,
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
-    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist);
-    BMH_LAUNCH(c, "mtf_first", k_mtf_first, dim3(nb, kFirstWG), kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_chist,
+    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist, d_firstc);
+    BMH_LAUNCH(c, "mtf_first", k_mtf_first, dim3(nb, kFirstWG), kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_firstc,
                d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
     if (h_first32) c->d2h(h_first32, d_first, (size_t)nb * 256 * 4);
