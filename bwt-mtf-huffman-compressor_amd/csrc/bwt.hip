@@ -556,43 +556,54 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
     }
 }
 
-// grid = nblocks; one thread per digit: per-chunk write offsets (block-relative, in place),
-// bucket table bk[b][d] = {start, len}; routing of buckets too big for a dense workgroup.
-__global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs,
-                                                     const uint32_t *__restrict__ bchunks,
-                                                     const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
+// The bucket scan in three launches so a block's chunk counts are walked by kG1ScanParts
+// workgroups instead of one (a small batch's few blocks left the single walk latency-bound:
+// 128 MiB 0.043 ms; at 1 GiB it is HBM-bound either way). Grid (nblocks, kG1ScanParts), one
+// thread per digit: part q of block b walks its chunks [q nq, q nq + nq) (list indices c0 + 8k,
+// the XCD lane stride), 32 loads in flight. k_g1_scan_sum: the part's digit counts.
+constexpr uint32_t kG1ScanParts = 4;
+__global__ __launch_bounds__(kG1Bins) void k_g1_scan_sum(const uint32_t *__restrict__ bchunks,
+                                                         const uint32_t *__restrict__ bchunk0,
+                                                         const uint32_t *__restrict__ chist, uint32_t *__restrict__ part)
+{
+    const uint32_t b = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
+    const uint32_t c0 = bchunk0[b], nc = bchunks[b], nq = (nc + kG1ScanParts - 1) / kG1ScanParts;
+    const uint32_t k0 = q * nq, k1 = min(nc, k0 + nq);
+    constexpr uint32_t U = 32;
+    uint32_t run = 0;
+    for (uint32_t k = k0; k < k1; k += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? chist[(size_t)(c0 + 8 * (k + j)) * kG1Bins + d] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) run += v[j];
+    }
+    part[((size_t)b * kG1ScanParts + q) * kG1Bins + d] = run;
+}
+
+// grid = nblocks; one thread per digit: the digit's total from the parts, the bucket table
+// bk[b][d] = {start, len}, each part's first write offset (in place over its count), and the
+// routing of buckets too big for a dense workgroup.
+__global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict__ boffs, uint32_t *__restrict__ part,
                                                      uint2 *__restrict__ bk, Seg4 *finb, Seg4 *big, Counters *cnt,
                                                      const uint32_t *__restrict__ loff, uint32_t big_cap,
                                                      const uint32_t *__restrict__ ainfo)
 {
     __shared__ uint32_t s_tmp[kG1Bins / 64 + 1];
     const uint32_t b = blockIdx.x, d = threadIdx.x;
-    const uint32_t c0 = bchunk0[b], nc = bchunks[b];  // list indices c0 + 8k (XCD lane stride)
-    // two sweeps over the block's chunk counts (32 loads in flight each: a small batch's few
-    // workgroups are latency-bound here): the digit's total, then, after the block scan, each
-    // chunk's write offset
-    constexpr uint32_t U = 32;
-    auto at = [&](uint32_t k) -> uint32_t & { return chist[(size_t)(c0 + 8 * k) * kG1Bins + d]; };
-    uint32_t run = 0;
-    for (uint32_t k = 0; k < nc; k += U) {
-        uint32_t v[U];
+    uint32_t *pp = part + (size_t)b * kG1ScanParts * kG1Bins + d;
+    uint32_t pv[kG1ScanParts], run = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < nc ? at(k + j) : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < U; ++j) run += v[j];
+    for (uint32_t q = 0; q < kG1ScanParts; ++q) {
+        pv[q] = pp[q * kG1Bins];
+        run += pv[q];
     }
     const uint32_t start = block_excl_sum<kG1Bins>(run, s_tmp, nullptr);
     uint32_t acc = start;
-    for (uint32_t k = 0; k < nc; k += U) {
-        uint32_t v[U];
 #pragma unroll
-        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < nc ? at(k + j) : 0u;
-#pragma unroll
-        for (uint32_t j = 0; j < U; ++j)
-            if (k + j < nc) {
-                at(k + j) = acc;
-                acc += v[j];
-            }
+    for (uint32_t q = 0; q < kG1ScanParts; ++q) {
+        pp[q * kG1Bins] = acc;
+        acc += pv[q];
     }
     bk[(size_t)b * kG1Bins + d] = make_uint2(start, run);
     const uint32_t x = b & 7u;  // the block's XCD lane sub-lists (parity 0)
@@ -605,6 +616,31 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
     else if (run > kDenseCap)
         finb[loff[kListFinb * 9 + x] + wave_append(&cnt->lc[0][kListFinb][x])] =
             make_uint4(boffs[b] + start, run, db, b);
+}
+
+// grid (nblocks, kG1ScanParts): per-chunk write offsets (block-relative, in place over the
+// chunk counts), part q from its first offset
+__global__ __launch_bounds__(kG1Bins) void k_g1_scan_offs(const uint32_t *__restrict__ bchunks,
+                                                          const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
+                                                          const uint32_t *__restrict__ part)
+{
+    const uint32_t b = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
+    const uint32_t c0 = bchunk0[b], nc = bchunks[b], nq = (nc + kG1ScanParts - 1) / kG1ScanParts;
+    const uint32_t k0 = q * nq, k1 = min(nc, k0 + nq);
+    constexpr uint32_t U = 32;
+    auto at = [&](uint32_t k) -> uint32_t & { return chist[(size_t)(c0 + 8 * k) * kG1Bins + d]; };
+    uint32_t acc = part[((size_t)b * kG1ScanParts + q) * kG1Bins + d];
+    for (uint32_t k = k0; k < k1; k += U) {
+        uint32_t v[U];
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? at(k + j) : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < U; ++j)
+            if (k + j < k1) {
+                at(k + j) = acc;
+                acc += v[j];
+            }
+    }
 }
 
 // Local counting sort of the chunk in LDS, then SA written in contiguous per-digit runs
@@ -2421,6 +2457,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     uint8_t *arank = (uint8_t *)(ainfo + nb);
     uint32_t *rlist = (uint32_t *)(arank + (size_t)nb * 256) + 1;
     uint2 *bk = (uint2 *)c->get(WS_BSTART, (size_t)nb * kG1Bins * 8);
+    uint32_t *g1part = (uint32_t *)c->get(WS_SCAN_PART, (size_t)nb * kG1ScanParts * kG1Bins * 4);
     const size_t seg_cap = N / 2 + 2;
     // every list entry covers >= 2 positions, so N / 2 entries bound every list; the finish
     // lists by size class and XCD lane (ccap, hloff above)
@@ -2501,8 +2538,12 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                        rlist);
             BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), 1024, 0, d_in, d_boffs,
                        d_chunks, rlist, chist, ainfo, arank, abits, 1u);
-            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, d_bchunks, d_bchunk0, chist, bk, lb[0],
-                       lg[0], d_cnt, d_loff, big_cap, ainfo);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_sum, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, chist,
+                       g1part);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, g1part, bk, lb[0], lg[0], d_cnt, d_loff,
+                       big_cap, ainfo);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_offs, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, chist,
+                       g1part);
         }
         pre_done = false;
         if (prologue_only) {

@@ -192,7 +192,9 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
     }
     {
         WallPhase w(c, "mtf");
+        c->mtf_dense = spec;
         mtf_batch(c, d_L, bt, d_mtf, nullptr, nullptr);
+        c->mtf_dense = false;
     }
     WallPhase wt(c, "huffman+pack");
     const uint32_t *d_prim = (const uint32_t *)c->get(WS_PRIMARY, nb * 4 + 64);

@@ -92,13 +92,15 @@ struct MChunk {
 // from 64l), then each symbol's rank = set bits above its last position (wave scan + one
 // popcount), and the symbol is stored at its rank.
 // (also resets what k_mtf_hist accumulates: the block histograms and first pack chunks; no
-// memset launches)
+// memset launches). kRuns: one atomicMax per run of equal symbols (text); batches found dense
+// (uniform-like bytes: no runs to save, and the check costs a third more VALU) take the plain loop.
+template <bool kRuns>
 __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__ L, const MChunk *__restrict__ chunks,
                                                      uint32_t nch, uint8_t *__restrict__ R, uint32_t *__restrict__ dcount,
                                                      uint32_t *__restrict__ freq, uint32_t *__restrict__ firstc,
                                                      uint32_t nfreq)
 {
-    __shared__ int lastpos[4][256];
+    __shared__ int lastpos[4][256 + (kRuns ? 64 : 0)];  // kRuns: + a sink slot per lane
     __shared__ uint32_t bset[4][kMtfChunk / 32];
     __shared__ uint32_t above[4][64];
     for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < nfreq; i += gridDim.x * 256) {
@@ -144,8 +146,8 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
 #pragma unroll
     for (uint32_t k = 0; k < 64; ++k) {
         const uint32_t x = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
-        const bool again = k + 1 < 64 && k + 1 < nv && ((sw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 255u) == x;
-        if (k < nv && !again) atomicMax(&lastpos[w][x], (int)(e0 + k));
+        const bool again = kRuns && k + 1 < 64 && k + 1 < nv && ((sw[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 255u) == x;
+        if (k < nv) atomicMax(&lastpos[w][again ? 256 + l : x], (int)(e0 + k));  // (repeats: the lane's sink)
     }
     wave_sync();
     uint32_t d = 0;
@@ -543,13 +545,16 @@ struct HChunk {
 // MTF stream). One workgroup per 64 K symbols of a block; wave w takes pack chunk w (lane l:
 // symbols [64l, 64l + 64), one 64-byte sector) with its own LDS histogram, no workgroup
 // barrier until the block totals. firstc[b][v] = the first pack chunk holding v (atomicMin over
-// the workgroups); the first occurrences inside those chunks come from k_mtf_first.
+// the workgroups, skipped when the value held is already smaller); the first occurrences inside
+// those chunks come from k_mtf_first. kRuns: MTF values 0 and 1 counted in registers (text).
+template <bool kRuns>
 __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ in, const HChunk *__restrict__ chunks,
                                                    const uint32_t *__restrict__ pfirst, uint32_t *__restrict__ freq,
                                                    uint16_t *__restrict__ chist, uint32_t *__restrict__ firstc)
 {
     constexpr uint32_t NW = 65536 / kPackChunkSyms;
     __shared__ uint32_t h[NW][256];
+    __shared__ uint32_t s_sink[kRuns ? NW : 1][64];
     const HChunk ch = chunks[blockIdx.x];
     const uint32_t t = threadIdx.x, w = t >> 6, l = t & 63u;
     const uint32_t s0 = w * kPackChunkSyms;
@@ -571,18 +576,24 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
             }
             // values 0 and 1 (most of a text block's MTF output) counted in a register: LDS
             // atomics on one address from many lanes serialise
-            uint32_t z01 = 0;
+            if (kRuns) {
+                // (branch-free: a 0 / 1 goes to the lane's own sink counter instead)
+                uint32_t z01 = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < 64; ++k) {
-                const uint32_t v = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
-                z01 += v < 2 ? 1u << (16 * v) : 0u;
-                if (v >= 2) atomicAdd(&h[w][v], 1u);
-            }
-            z01 = wave_sum_dpp(z01);  // <= 4096 per value: two 16-bit fields
-            wave_sync();
-            if (l == 0) {
-                h[w][0] += z01 & 0xffffu;
-                h[w][1] += z01 >> 16;
+                for (uint32_t k = 0; k < 64; ++k) {
+                    const uint32_t v = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
+                    z01 += v < 2 ? 1u << (16 * v) : 0u;
+                    atomicAdd(v < 2 ? &s_sink[w][l] : &h[w][v], 1u);
+                }
+                z01 = wave_sum_dpp(z01);  // <= 4096 per value: two 16-bit fields
+                wave_sync();
+                if (l == 0) {
+                    h[w][0] += z01 & 0xffffu;
+                    h[w][1] += z01 >> 16;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < 64; ++k) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
             }
         } else {
             for (uint32_t k = 0; k < 64 && e0 + k < len; ++k) atomicAdd(&h[w][in[a + e0 + k]], 1u);
@@ -602,7 +613,9 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
         }
         if (tot) {
             atomicAdd(&freq[(size_t)ch.block * 256 + t], tot);
-            atomicMin(&firstc[(size_t)ch.block * 256 + t], ch.rel / kPackChunkSyms + fx);
+            uint32_t *fp = &firstc[(size_t)ch.block * 256 + t];
+            const uint32_t cand = ch.rel / kPackChunkSyms + fx;
+            if (cand < __atomic_load_n(fp, __ATOMIC_RELAXED)) atomicMin(fp, cand);  // values only fall
         }
     }
 }
@@ -835,7 +848,12 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     uint32_t *d_freq = (uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     uint32_t *d_first = (uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 8);
     uint32_t *d_firstc = d_first + (size_t)nb * 256;  // first pack chunk of each value (k_mtf_hist)
-    BMH_LAUNCH(c, "mtf_recency", k_mtf_recency, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount, d_freq,
+    const bool runs = !c->mtf_dense;  // (Ctx::mtf_dense: the batch's digram census found it dense)
+    if (runs)
+        BMH_LAUNCH(c, "mtf_recency", k_mtf_recency<true>, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount,
+                   d_freq, d_firstc, nb * 256);
+    else
+        BMH_LAUNCH(c, "mtf_recency", k_mtf_recency<false>, (nch + 3) / 4, 256, 0, d_L, d_chunks, nch, d_R, d_dcount, d_freq,
                d_firstc, nb * 256);
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<false, true>), ng, 64, 0, d_r1, d_R, d_dcount, nullptr, nullptr, d_Rg,
                d_dg);
@@ -853,7 +871,10 @@ void mtf_batch(Ctx *c, const uint8_t *d_L, const Batch &bt, uint8_t *d_mtf, uint
     BMH_LAUNCH(c, "mtf_compose", (k_mtf_compose<true, false>), ng, 64, 0, d_r3, d_R, d_dcount, d_Sg, d_S, nullptr,
                nullptr);
     BMH_LAUNCH(c, "mtf_encode", k_mtf_encode, (nch + kLanes - 1) / kLanes, kLanes, 0, d_L, d_chunks, nch, d_S, d_mtf);
-    BMH_LAUNCH(c, "mtf_hist", k_mtf_hist, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist, d_firstc);
+    if (runs)
+        BMH_LAUNCH(c, "mtf_hist", k_mtf_hist<true>, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist, d_firstc);
+    else
+        BMH_LAUNCH(c, "mtf_hist", k_mtf_hist<false>, nhh, 1024, 0, d_mtf, d_hh, d_pfirst, d_freq, d_chist, d_firstc);
     BMH_LAUNCH(c, "mtf_first", k_mtf_first, dim3(nb, kFirstWG), kFirstNT, 0, d_mtf, d_boffs, d_pfirst, d_freq, d_firstc,
                d_first);
     if (h_freq32) c->d2h(h_freq32, d_freq, (size_t)nb * 256 * 4);
