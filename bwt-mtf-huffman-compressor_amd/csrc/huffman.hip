@@ -465,10 +465,14 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
 }
 
 // One workgroup: record offsets = exclusive scan of (header + payload) sizes.
+// hdr non-null (batches of <= kRecHdrFused blocks): the same workgroup then copies the headers
+// (wave w: blocks w, w + 16, ...), so a latency-bound batch saves the k_rec_headers launch
+constexpr uint32_t kRecHdrFused = 256;
 __global__ __launch_bounds__(1024) void k_rec_offs(uint32_t nb, const uint32_t *__restrict__ hdr_len,
                                                    const uint64_t *__restrict__ pay_bytes, uint64_t *__restrict__ roffs,
                                                    uint64_t *__restrict__ pay_offs, uint64_t out_cap, uint32_t *status,
-                                                   const uint64_t *base)
+                                                   const uint64_t *base, const uint8_t *__restrict__ hdr,
+                                                   uint8_t *__restrict__ out)
 {
     __shared__ uint64_t s_tmp[17];
     uint64_t carry = base ? *base : 0ull;  // sub-batches chain on the previous one's end
@@ -486,6 +490,14 @@ __global__ __launch_bounds__(1024) void k_rec_offs(uint32_t nb, const uint32_t *
     if (threadIdx.x == 0) {
         roffs[nb] = carry;
         if (carry > out_cap) atomicOr(status, kStatusCapacity);
+    }
+    if (!hdr || carry > out_cap) return;  // (workgroup-uniform: every thread holds the total)
+    __syncthreads();                      // roffs of every block written
+    const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63u;
+    for (uint32_t b = w; b < nb; b += 16) {
+        const uint8_t *h = hdr + (size_t)b * kHdrStride;
+        uint8_t *o = out + roffs[b];
+        for (uint32_t i = l; i < hdr_len[b]; i += 64) o[i] = h[i];
     }
 }
 
@@ -580,7 +592,9 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         BMH_HIP(hipStreamWaitEvent(c->stream, chain->ev[sub - 1], 0));
         d_base = chain->d_end[sub - 1];
     }
-    BMH_LAUNCH(c, "rec_offs", k_rec_offs, 1, 1024, 0, nb, d_hlen, d_payb, d_roffs, d_pay_offs, out_cap, d_status, d_base);
+    const bool fused = nb <= kRecHdrFused;
+    BMH_LAUNCH(c, "rec_offs", k_rec_offs, 1, 1024, 0, nb, d_hlen, d_payb, d_roffs, d_pay_offs, out_cap, d_status, d_base,
+               fused ? d_hdr : nullptr, d_out);
     if (chain) {
         BMH_HIP(hipEventRecord(chain->ev[sub], c->stream));
         {
@@ -590,7 +604,7 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         }
         chain->cv.notify_all();
     }
-    BMH_LAUNCH(c, "rec_headers", k_rec_headers, nb, 64, 0, d_hdr, d_hlen, d_roffs, d_out, d_status);
+    if (!fused) BMH_LAUNCH(c, "rec_headers", k_rec_headers, nb, 64, 0, d_hdr, d_hlen, d_roffs, d_out, d_status);
 }
 
 }  // namespace bmh
