@@ -1025,3 +1025,40 @@ def test_planted_ties_in_large_batch(ctx, oracle):
         assert prim == oprim and L == oL, i
     for r, d in zip(recs, blocks):
         assert ctx.decompress_bytes(r) == d
+
+
+def test_speculative_round_with_run_heavy_block(ctx, oracle):
+    """A dense batch (11 random 4 MiB blocks) that also holds a 1 MiB run-heavy block (runs of
+    4..12 bytes: <= n / 4 runs): one pipeline with the speculative list round for the sorter
+    blocks, while the screen sends the run-heavy block to the run path on the side stream; no
+    fallback, every record the reference's."""
+    bs, nr = 4 << 20, 11
+    rng = np.random.default_rng(31)
+    vals = rng.integers(0, 256, 200000, dtype=np.uint8)
+    lens = rng.integers(4, 13, 200000)
+    run_blk = np.repeat(vals, lens)[: 1 << 20].tobytes()
+    sizes = [bs] * 5 + [len(run_blk)] + [bs] * 6
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    d_in = ctx.alloc(int(offs[-1]))
+    g = 0
+    for i, n in enumerate(sizes):
+        if i == 5:
+            d_in.upload(np.frombuffer(run_blk, np.uint8), offset=int(offs[i]))
+        else:
+            ctx.synth_splitmix64(d_in.ptr.value + int(offs[i]), bs, 0, g * bs)
+            g += 1
+    cap = sum(int(bmh.lib().bmh_record_bound(n)) for n in sizes)
+    d_out = ctx.alloc(cap)
+    f0 = ctx.spec_fallbacks()
+    ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
+    assert ctx.last_pipelines() == 1 and ctx.spec_fallbacks() == f0
+    recs = d_out.download(int(ro[-1])).tobytes()
+    man = manifest("random_1g_4m")["blocks"]
+    g = 0
+    for i in range(len(sizes)):
+        r = recs[int(ro[i]):int(ro[i + 1])]
+        if i == 5:
+            assert r == oracle.encode(run_blk)
+        else:
+            assert hashlib.sha256(r).hexdigest() == man[g]["sha256"], i
+            g += 1
