@@ -1,6 +1,6 @@
 #!/bin/bash
 # Calgary whole-file batch: kernel timeline of one call (default pipelines)
-o=gpurun_out/${TAG:-r5y}; mkdir -p $o
+o=gpurun_out/${TAG:-caltl}; mkdir -p $o
 export TMPDIR=/tmp
 files="bib book1 book2 geo news obj1 obj2 paper1 paper2 pic progc progl progp trans"
 timeout -k 10 120 rocprofv3 --kernel-trace -d $o/t -o run --output-format csv -- python3 tools/cal_trace_run.py $files > $o/log 2>&1 || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # dense-finish phase ticks on text (config 3 and 16 MiB blocks) and random data, then the GPU
 # suite and the text configs on the in-tree library
-o=gpurun_out/${TAG:-r5dp}; mkdir -p $o
+o=gpurun_out/${TAG:-dphase}; mkdir -p $o
 export TMPDIR=/tmp
 for cfg in "100 1" "128 16"; do
   BMH_LIB=variants/denseprof/libbmh.so timeout -k 10 150 python3 tools/text_bench.py $cfg pipelines=1 > $o/dp_${cfg// /_}.json 2> $o/dp_${cfg// /_}.err || exit 1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU suite, then text configs and random 1 GiB / 128 MiB alternating over library builds
-o=gpurun_out/${TAG:-r5sm}; mkdir -p $o
+o=gpurun_out/${TAG:-textab}; mkdir -p $o
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $o/tests.log 2>&1
 rc=$?; tail -2 $o/tests.log; [ $rc -eq 0 ] || exit $rc
