@@ -122,6 +122,7 @@ struct Ctx {
     uint64_t pre_sig = 0;  // bwt_batch_core's prologue already launched for this input + layout
     bool spec_lists = false, spec_pending = false;
     bool mtf_dense = false;  // the batch was found dense: MTF stages skip their run-aware paths
+    std::vector<uint64_t> roffs_host;  // encode_blocks_one: record offsets + status, one copy
     uint32_t spec_fallbacks = 0;
     uint32_t spec_cnt[128] = {};  // the list counters after the speculative round
     // host-buffer streaming (capi.cpp): copy streams and two pinned staging slots each way

@@ -201,8 +201,9 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
     const uint32_t *d_freq = (const uint32_t *)c->get(WS_FREQ, (size_t)nb * 256 * 4);
     const uint32_t *d_first = (const uint32_t *)c->get(WS_FIRST, (size_t)nb * 256 * 4);
     DevTable *d_tabs = (DevTable *)c->get(WS_TABLES, nb * sizeof(DevTable));
-    uint64_t *d_roffs = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 1) * 8 + 64);
-    uint64_t *d_pay_offs = d_roffs + nb + 1;
+    // record offsets [0, nb] | the batch's status word (k_rec_offs) | payload offsets
+    uint64_t *d_roffs = (uint64_t *)c->get(WS_ROFFS, (size_t)(2 * nb + 2) * 8 + 64);
+    uint64_t *d_pay_offs = d_roffs + nb + 2;
     uint8_t *d_misc = (uint8_t *)c->get(WS_STATUS, (size_t)(nb + 1) * 8 + 64);
     uint32_t *d_status = (uint32_t *)d_misc;
     uint64_t *d_boffs = (uint64_t *)(d_misc + 64);
@@ -218,10 +219,12 @@ static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint
                    sub);
     const uint16_t *d_chist = (const uint16_t *)c->get(WS_PACK_HIST, 64);  // written by mtf_batch
     pack_batch_dev(c, d_mtf, bt, d_tabs, d_pay_offs, d_out, d_status, d_chist);
-    uint32_t st = 0;
-    c->d2h(rec_offs, d_roffs, (nb + 1) * 8);
-    c->d2h(&st, d_status, 4);
+    std::vector<uint64_t> &ro = c->roffs_host;  // offsets and status in one copy
+    ro.resize(nb + 2);
+    c->d2h(ro.data(), d_roffs, (nb + 2) * 8);
     c->sync();
+    memcpy(rec_offs, ro.data(), (nb + 1) * 8);
+    const uint32_t st = (uint32_t)ro[nb + 1];
     if (st) {  // keep the status word zero for the next batch
         BMH_HIP(hipMemsetAsync(d_status, 0, 4, c->stream));
         c->sync();

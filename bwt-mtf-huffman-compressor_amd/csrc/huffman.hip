@@ -490,6 +490,9 @@ __global__ __launch_bounds__(1024) void k_rec_offs(uint32_t nb, const uint32_t *
     if (threadIdx.x == 0) {
         roffs[nb] = carry;
         if (carry > out_cap) atomicOr(status, kStatusCapacity);
+        // the batch's final status (k_huff_build's bits + capacity) beside the offsets: the host
+        // reads both with one copy (nothing later in the encode sets status bits)
+        roffs[nb + 1] = *(volatile uint32_t *)status | (carry > out_cap ? kStatusCapacity : 0u);
     }
     if (!hdr || carry > out_cap) return;  // (workgroup-uniform: every thread holds the total)
     __syncthreads();                      // roffs of every block written
