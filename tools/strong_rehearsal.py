@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import subprocess
 import sys
 
@@ -51,14 +52,16 @@ def main() -> None:
             print(f"N={n} per-rank {mib} MiB: {x['ms_per_step']} ms, streams {x['streams_per_gpu']}, "
                   f"kernels {x['kernel_sum_ms']} ms, pcie {x['pcie_ms_per_step']} ms, {x['parity']}", flush=True)
         rows[n] = {"per_rank_mib": mib, "runs": reps,
-                   "median_ms": sorted(x["ms_per_step"] for x in reps)[len(reps) // 2],
-                   "median_pcie_ms": (sorted(x["pcie_ms_per_step"] for x in reps)[len(reps) // 2]
+                   "median_ms": round(statistics.median(x["ms_per_step"] for x in reps), 4),
+                   "min_ms": min(x["ms_per_step"] for x in reps),
+                   "median_pcie_ms": (statistics.median(x["pcie_ms_per_step"] for x in reps)
                                       if a.pcie_steps else None)}
-    t1 = rows[1]["median_ms"]
+    t1, m1 = rows[1]["median_ms"], rows[1]["min_ms"]
     for n, row in rows.items():
         t = row["median_ms"]
         row["predicted_value_MBps"] = round((1 << 30) / (t / 1e3) / 1e6, 1)
         row["predicted_efficiency"] = round(t1 / (n * t), 3)
+        row["predicted_efficiency_min"] = round(m1 / (n * row["min_ms"]), 3)  # fastest process each
         row["cost_vs_ideal"] = round(t / (t1 / n), 3)
         if row["median_pcie_ms"]:
             p1 = rows[1]["median_pcie_ms"]
