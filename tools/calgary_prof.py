@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Kernel / host-wall breakdown of the Calgary encode (BASELINE configs 1-2) on one GPU:
-python tools/calgary_prof.py [--mode whole|256k] [--steps 5]. Prints one JSON line."""
+python tools/calgary_prof.py [--mode whole|256k] [--steps 5] [--opts name=value,...]. Prints one JSON line."""
 import argparse
 import json
 import os
@@ -18,9 +18,11 @@ CAL = ["bib", "book1", "book2", "geo", "news", "obj1", "obj2", "paper1", "paper2
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", default="whole", choices=["whole", "256k", "each"])
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--opts", default="", help="bmh_ctx_set_option list name=value,...")
 a = ap.parse_args()
 datas = [open(os.path.join(REPO, "tests", "golden", "calgary", f), "rb").read() for f in CAL]
 ctx = bmh.Context(0)
+ctx.set_options(a.opts)
 
 
 def run(blocks, steps):
