@@ -958,7 +958,8 @@ def test_speculative_list_round_fallback(ctx, oracle):
     counters at the end (bwt.hip bwt_spec_ok): a 48 MiB random batch needs no fallback (records
     = the config-4 manifest's); the same batch with a 2 KB stretch of block 5 repeated inside the
     block (rotations tied for up to 16 K bits: more list rounds, then rank doubling) falls back
-    once and its records equal the reference's; then a clean batch speculates again."""
+    once and its records equal the reference's; then a clean batch speculates again; then 400 tied
+    pairs in one lane (past the speculative grid) fall back once more."""
     bs, nblk = 4 << 20, 12
     offs = np.arange(nblk + 1, dtype=np.uint64) * np.uint64(bs)
     d_in = ctx.alloc(bs * nblk)
@@ -991,6 +992,17 @@ def test_speculative_list_round_fallback(ctx, oracle):
     recs = run()
     assert ctx.spec_fallbacks() == f0 + 1
     assert hashlib.sha256(recs[5]).hexdigest() == man[5]["sha256"]
+    # more tied pairs in one XCD lane than the speculative grid covers (256 entries): 400
+    # 12-byte copies in block 5 (each pair resolved in the one tiny round) -> one fallback
+    blk = bytearray(synth.splitmix64_bytes(0, 5 * bs, bs).tobytes())
+    rng = np.random.default_rng(3)
+    for src in rng.choice(np.arange(0, bs // 2 - 64, 64), 400, replace=False):
+        dst = int(src) + bs // 2
+        blk[dst:dst + 12] = blk[int(src):int(src) + 12]
+    d_in.upload(np.frombuffer(bytes(blk), np.uint8), offset=5 * bs)
+    recs = run()
+    assert ctx.spec_fallbacks() == f0 + 2
+    assert recs[5] == oracle.encode(bytes(blk))
 
 
 def test_planted_ties_in_large_batch(ctx, oracle):
