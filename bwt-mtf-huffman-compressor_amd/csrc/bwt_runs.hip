@@ -52,9 +52,10 @@ constexpr uint32_t kMask24 = (1u << 24) - 1;
 static_assert(kRunScreenMax / kRunShare <= kRunRankLimit, "a screened batch's runs fit the 24-bit rank field");
 
 // Digram census (dense_batch): distinct byte pairs among the first kProbeSample positions of each
-// block, one workgroup a block, a 65 536-bit LDS bitmap. Uniform-random bytes give ~14.5 K
-// distinct pairs in 16 K positions, text a few hundred to a few thousand.
-constexpr uint32_t kProbeSample = 16384, kProbeNT = 1024;
+// block, one workgroup a block, a 65 536-bit LDS bitmap. Uniform-random bytes give ~3 970
+// distinct pairs in 4 K positions, text a few hundred (16 K samples: the same split at twice the kernel time, 10.6 vs
+// 5.2 us for 32 blocks).
+constexpr uint32_t kProbeSample = 4096, kProbeNT = 1024;
 // boffs null: block b is [b * bs, b * bs + bs). out: pinned host memory (vector stores).
 __global__ __launch_bounds__(kProbeNT) void k_probe_digrams(const uint8_t *__restrict__ in,
                                                             const uint64_t *__restrict__ boffs, uint64_t bs,
@@ -681,7 +682,7 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
 
 // Whether a batch is dense (uniform-like bytes: the BWT's two data passes resolve it with one
 // short list round, no host-synchronised rounds), by the digram census of each block's first
-// 16 K positions: at least half of the sampled pairs distinct, for blocks holding >= 90 % of the
+// 4 K positions: at least half of the sampled pairs distinct, for blocks holding >= 90 % of the
 // bytes. encode_blocks runs such batches on one pipeline: on random data the pipelines only
 // contend (128 MiB: 1.77 ms on one, 1.99 on four). One launch (1024 threads a block; block
 // offsets from the block size when the blocks are equal) whose counts land in pinned memory,
