@@ -53,8 +53,8 @@ static_assert(kRunScreenMax / kRunShare <= kRunRankLimit, "a screened batch's ru
 
 // Digram census (dense_batch): distinct byte pairs among the first kProbeSample positions of each
 // block, one workgroup a block, a 65 536-bit LDS bitmap. Uniform-random bytes give ~3 970
-// distinct pairs in 4 K positions, text a few hundred (16 K samples: the same split at twice the kernel time, 10.6 vs
-// 5.2 us for 32 blocks).
+// distinct pairs in 4 K positions, text a few hundred (16 K samples: the same split at twice
+// the kernel time, 10.6 vs 5.2 us for 32 blocks).
 constexpr uint32_t kProbeSample = 4096, kProbeNT = 1024;
 // boffs null: block b is [b * bs, b * bs + bs). out: pinned host memory (vector stores).
 __global__ __launch_bounds__(kProbeNT) void k_probe_digrams(const uint8_t *__restrict__ in,
