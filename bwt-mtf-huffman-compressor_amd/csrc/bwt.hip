@@ -987,6 +987,7 @@ __device__ __forceinline__ void finish_core(const DataArgs &a, uint32_t gstart, 
 // per segment would leave most lanes idle.
 // epw = list entries per wave (64, or 16 / 32 when a round's tiny list is short: a wave walks
 // its entries' rotations in rounds of 64, so short lists finish sooner spread over more waves)
+constexpr uint32_t kTinyPairExt = 4;
 __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__restrict__ lists,
                                                      const uint32_t *__restrict__ loff, const uint32_t *__restrict__ cnt,
                                                      LaneMap lm, uint32_t epw)
@@ -1048,8 +1049,28 @@ __global__ __launch_bounds__(256) void k_finish_tiny(DataArgs a, const Seg4 *__r
                     eqt += m && kj == key;
                     eqb += m && kj == key && j < idx;
                 }
+                uint64_t newbits = (uint64_t)db + 64;
+                // a tied pair (the common text case) looks further right here, up to kTinyPairExt
+                // windows, instead of going round the deferred list again
+                bool pt = live && len == 2 && eqt == 2 && newbits < 8ull * n;
+                for (uint32_t it = 0; it < kTinyPairExt && __ballot(pt); ++it) {  // wave-uniform
+                    const uint64_t k2 = pt ? rot_window(blk, n, p, newbits) : 0ull;
+                    const int src = (int)(pos + (idx ^ 1u));
+                    const uint32_t plo = __shfl((uint32_t)k2, src, 64), phi = __shfl((uint32_t)(k2 >> 32), src, 64);
+                    const uint64_t kp = ((uint64_t)phi << 32) | plo;
+                    if (pt) {
+                        if (kp != k2) {
+                            lt = kp < k2;
+                            eqb = 0;
+                            eqt = 1;
+                            pt = false;
+                        } else {
+                            newbits += 64;
+                            pt = newbits < 8ull * n;
+                        }
+                    }
+                }
                 if (live) {
-                    const uint64_t newbits = (uint64_t)db + 64;
                     const bool final_depth = newbits >= 8ull * n;
                     const uint32_t slot = gstart + lt + eqb, gs = gstart + lt;
                     if (eqt > 1 && eqb == 0)

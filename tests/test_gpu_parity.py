@@ -1039,6 +1039,33 @@ def test_planted_ties_in_large_batch(ctx, oracle):
         assert ctx.decompress_bytes(r) == d
 
 
+def test_tied_pairs_across_windows(ctx, oracle):
+    """Tied pairs whose shared prefix ends inside each of the first windows the tiny list pass
+    looks at (it extends a tied pair up to 4 windows of 64 bits before deferring it): a random
+    1 MiB block with substrings of 9..80 bytes copied once each, one copied across the block end
+    (the rotation wraps), plus small blocks whose rotations all tie to the final depth (period
+    n / 2). BWT equals the oracle's and every record decodes back."""
+    rng = np.random.default_rng(2025)
+    bs = 1 << 20
+    a = rng.integers(0, 256, bs, dtype=np.uint8)
+    at = 4096
+    for ln in (9, 15, 16, 17, 24, 31, 32, 33, 40, 41, 48, 56, 63, 64, 65, 72, 80):
+        src = int(rng.integers(0, bs - 100))
+        a[at:at + ln] = a[src:src + ln]
+        at += 3000
+    a[bs - 20:] = a[500:520]  # the rotation at bs - 20 matches 20 bytes, then wraps to a[0:]
+    a[0:30] = a[520:550]
+    per = rng.integers(0, 256, 50, dtype=np.uint8)
+    blocks = [a.tobytes(), np.tile(per, 2).tobytes(), np.tile(per[:7], 2).tobytes(),
+              rng.integers(0, 4, 300, dtype=np.uint8).tobytes()]
+    for blk in blocks:
+        prim, L = bmh.bwt(blk, ctx)
+        oprim, oL = oracle.bwt(blk)
+        assert prim == oprim and L == oL, len(blk)
+    for r, d in zip(ctx.encode_blocks(blocks), blocks):
+        assert ctx.decompress_bytes(r) == d
+
+
 def test_speculative_round_with_run_heavy_block(ctx, oracle):
     """A dense batch (11 random 4 MiB blocks) that also holds a 1 MiB run-heavy block (runs of
     4..12 bytes: <= n / 4 runs): one pipeline with the speculative list round for the sorter
