@@ -119,6 +119,8 @@ struct Ctx {
     hipEvent_t probe_ev = nullptr;
     uint32_t *run_cnt_host = nullptr;  // run path: doubling rounds' group counts (pinned), read one round late
     hipEvent_t run_ev[2] = {};
+    void *dbl_cnt_host = nullptr;  // rank doubling: two rounds' counters (pinned), read one round late
+    hipEvent_t dbl_ev[2] = {};
     uint64_t pre_sig = 0;  // bwt_batch_core's prologue already launched for this input + layout
     bool spec_lists = false, spec_pending = false;
     bool mtf_dense = false;  // the batch was found dense: MTF stages skip their run-aware paths

@@ -2819,14 +2819,24 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
         };
         classify(seg_cur, 0, cnt_of(1));
         read_counters();
-        uint32_t ncur = h_cnt->next;
-        uint64_t D = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
-        int round = 0;
-        // One host wait per round (the next round's segment count and termination): every
-        // kernel of a round reads its list lengths from the device counters and strides over
-        // them with a fixed grid; the large path's tiles are built on the device (k_tiles).
-        while (ncur > 0) {
-            if (D == 0) fail(BMH_EHIP, "bwt: internal error (zero doubling depth)");
+        const uint32_t ncur0 = h_cnt->next;
+        const uint64_t D0 = h_cnt->dmin_bits / 8;  // every tied group shares at least D bytes
+        if (ncur0 > 0 && D0 == 0) fail(BMH_EHIP, "bwt: internal error (zero doubling depth)");
+        // Every kernel of a round reads its list lengths from the device counters and strides
+        // over them with a fixed grid; the large path's tiles are built on the device (k_tiles).
+        // The host reads each round's counters one round late: round r + 1 is queued before the
+        // wait for round r's, so the GPU never idles on the wait; the one round queued past the
+        // last finds no segments and leaves everything as it was. A round launched before its
+        // counters are known runs the tiny and medium kernels (empty lists exit at once) and the
+        // large passes if the round before it had large segments (groups only split, so a
+        // large segment's parent was large).
+        if (!c->dbl_cnt_host) BMH_HIP(hipHostMalloc(&c->dbl_cnt_host, 2 * sizeof(Counters), hipHostMallocDefault));
+        for (auto &e : c->dbl_ev)
+            if (!e) BMH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        Counters *hc = (Counters *)c->dbl_cnt_host;
+        uint2 *seg_in[2] = {seg_cur, seg_nxt};
+        auto launch_round = [&](int round, uint64_t D, bool has_large, bool run_tiny, bool run_med) {
+            uint2 *seg_out = seg_in[(round + 1) & 1];
             RoundArgs a;
             a.data = d_in;
             a.boffs = d_boffs;
@@ -2839,12 +2849,12 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             a.rk_nxt = odd ? rkA : rkB;
             a.D = (uint32_t)std::min<uint64_t>(D, 0xffffffffull);
             a.newD = 2 * D;
-            a.next = seg_nxt;
+            a.next = seg_out;
             a.resolved = resolved;
             a.cnt = d_cnt;
             a.next_cnt = cnt_of(round + 1);
 
-            const bool has_large = h_cnt->large != 0;  // the large path also appends tiny / medium segments
+            // (the large path also appends tiny / medium segments)
             for (uint32_t pass = 0; has_large && pass < npass; ++pass) {  // passes with no segments exit at once
                 uint32_t *cnt_in = pass & 1 ? &d_cnt->large_next : &d_cnt->large;
                 uint32_t *cnt_out = pass & 1 ? &d_cnt->large : &d_cnt->large_next;
@@ -2860,18 +2870,33 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                 BMH_LAUNCH(c, "bwt_lcopy", k_lcopy, kDblGrid, 256, 0, d_ltiles, &d_cnt->ltiles, d_lnomove, sa, key, sa2,
                            key2);
             }
-            if (has_large || h_cnt->tiny) BMH_LAUNCH(c, "bwt_tiny", k_dtiny, kDblGrid, 256, 0, a, tiny);
-            if (has_large || h_cnt->med) BMH_LAUNCH(c, "bwt_medium", k_medium, kDblGrid, kMedNT, 0, a, med);
+            if (has_large || run_tiny) BMH_LAUNCH(c, "bwt_tiny", k_dtiny, kDblGrid, 256, 0, a, tiny);
+            if (has_large || run_med) BMH_LAUNCH(c, "bwt_medium", k_medium, kDblGrid, kMedNT, 0, a, med);
             BMH_LAUNCH(c, "bwt_groups", k_groups, kDblGrid, 256, 0, a, groups, gcoop);
             BMH_LAUNCH(c, "bwt_groups", k_groups_coop, kCoopGrid, 256, 0, a, groups, gcoop);
             BMH_LAUNCH(c, "bwt_commit", k_commit, kDblGrid, 256, 0, resolved, &d_cnt->resolved, a.rk_nxt,
                        (uint32_t *)a.rk_cur);
-            classify(seg_nxt, round + 1, cnt_of(round));
-            read_counters();
-            ncur = (round & 1) ? h_cnt->next : h_cnt->next2;  // in(round + 1)
-            std::swap(seg_cur, seg_nxt);
-            D = a.newD;
-            ++round;
+            classify(seg_out, round + 1, cnt_of(round));
+            BMH_HIP(hipMemcpyAsync(hc + (round & 1), d_cnt, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+            BMH_HIP(hipEventRecord(c->dbl_ev[round & 1], c->stream));
+        };
+        if (ncur0 > 0) {
+            uint64_t D = D0;
+            launch_round(0, D, h_cnt->large != 0, h_cnt->tiny != 0, h_cnt->med != 0);
+            bool large_ub = h_cnt->large != 0;  // round r - 1's counters: a bound for round r + 1
+            for (int round = 0;; ++round) {
+                launch_round(round + 1, 2 * D, large_ub, true, true);
+                for (;;) {  // spin: a blocking wait can sleep the host thread for milliseconds
+                    const hipError_t e = hipEventQuery(c->dbl_ev[round & 1]);
+                    if (e == hipSuccess) break;
+                    if (e != hipErrorNotReady) BMH_HIP(e);
+                }
+                const Counters &cr = hc[round & 1];
+                const uint32_t ncur = (round & 1) ? cr.next : cr.next2;  // in(round + 1)
+                large_ub = cr.large != 0;
+                if (ncur == 0) break;  // round + 1 (queued) had nothing to do
+                D *= 2;
+            }
         }
     }
 

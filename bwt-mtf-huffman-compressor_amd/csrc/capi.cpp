@@ -867,6 +867,9 @@ void bmh_ctx_destroy(bmh_ctx *c)
     if (c->run_cnt_host) (void)hipHostFree(c->run_cnt_host);
     for (auto e : c->run_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->dbl_cnt_host) (void)hipHostFree(c->dbl_cnt_host);
+    for (auto e : c->dbl_ev)
+        if (e) (void)hipEventDestroy(e);
     for (int s = 0; s < WS_COUNT_; ++s)
         if (c->ws[s]) (void)hipFree(c->ws[s]);
     if (c->pinned) (void)hipHostFree(c->pinned);
