@@ -21,6 +21,10 @@ for r in $(seq $rounds); do
     done
     BMH_LIB=$lib timeout -k 10 120 python3 tools/calgary_prof.py --mode whole --steps 10 > $o/${n}_cal_$r.json 2>/dev/null || exit 1
     BMH_LIB=$lib timeout -k 10 120 python3 tools/calgary_prof.py --mode 256k --steps 10 > $o/${n}_c256_$r.json 2>/dev/null || exit 1
+    if [ -n "$BENCH" ]; then  # BENCH=1: the 1 GiB headline step too
+      BMH_LIB=$lib timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --decode-steps 0 --pcie-steps 0 --calgary-steps 0 2>/dev/null | tail -1 > $o/${n}_b_$r.json || exit 1
+      python3 -c "import json; print('   1GiB', json.load(open('$o/${n}_b_$r.json'))['ms_per_step'])"
+    fi
     python3 - $o $n $r $l <<'P'
 import json, sys
 o, n, r, l = sys.argv[1:]
