@@ -187,7 +187,7 @@ __global__ __launch_bounds__(1024) void k_tiles_excl(const uint32_t *__restrict_
 // rank. The scatter takes its digit offsets from the counts of the tiles before it (up to
 // kRsInlineTiles tiles: two launches a pass), or from a per-digit scan (k_rsort_rows) beyond.
 constexpr uint32_t kRsBits = 11, kRsBins = 1u << kRsBits, kRsDPT = kRsBins / 256;  // digits per thread
-constexpr uint32_t kRsTile = 4096, kRsInlineTiles = 16;  // inline: each tile reads kRsBins x tiles counts
+constexpr uint32_t kRsTile = 4096, kRsInlineTiles = 4;  // inline: each tile reads kRsBins x tiles counts
 __global__ __launch_bounds__(256) void k_rsort_hist(const uint64_t *__restrict__ key, uint32_t n, uint32_t shift,
                                                     uint32_t ntiles, uint32_t *__restrict__ cnt, const uint32_t *gate)
 {

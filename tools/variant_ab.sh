@@ -16,6 +16,13 @@ for r in $(seq $rounds); do
   for l in "$@"; do
     lib=$l; [ "$l" = "." ] && lib=bwt-mtf-huffman-compressor_amd/lib/libbmh.so
     n=$(echo $l | tr '/.' '__')
+    if [ -n "$CAL_ONLY" ]; then  # CAL_ONLY=1: Calgary only
+      for m in whole 256k; do
+        BMH_LIB=$lib timeout -k 10 120 python3 tools/calgary_prof.py --mode $m --steps 10 > $o/${n}_${m}_$r.json 2>/dev/null || exit 1
+      done
+      python3 -c "import json; print('$l'.ljust(26), 'calgary whole/256k', [json.load(open('$o/${n}_'+m+'_$r.json'))['ms'] for m in ('whole', '256k')])"
+      continue
+    fi
     for cfg in "100 1" "128 16" "128 4"; do
       BMH_LIB=$lib timeout -k 10 150 python3 tools/text_bench.py $cfg > $o/${n}_t${cfg// /_}_$r.json || exit 1
     done
