@@ -48,7 +48,7 @@ constexpr uint32_t kMtfChunk = 4096;  // symbols per lane (one chunk)
 // of 4096.
 // BMH_OPT_MTF_CHUNK (bmh_ctx_set_option) overrides it for experiments.
 constexpr uint32_t kMtfChunkMin = 256;
-constexpr uint32_t kMtfWgPerCu = 6;  // k_mtf_encode: 23.5 KB of LDS per one-wave workgroup
+constexpr uint32_t kMtfWgPerCu = 7;  // k_mtf_encode: 22 KB of LDS per one-wave workgroup
 static uint64_t mtf_chunk_count(const Batch &bt, uint64_t x)
 {
     uint64_t k = 0;
@@ -78,7 +78,6 @@ static uint32_t mtf_chunk_len(Ctx *c, const Batch &bt)
     return (uint32_t)x;
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
-constexpr int kMtfAhead = 1;  // symbols whose stamp reads run ahead of the update
 
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
@@ -280,153 +279,137 @@ __global__ __launch_bounds__(64) void k_mtf_compose(const CRun *__restrict__ run
     }
 }
 
-// Per-lane encode state, in one LDS array of dword rows; row k of lane l is the dword at
-// byte k * 256 + 4 * l, so every lane stays in its own bank:
-//   rows  0..63  stamp bytes: the low 8 bits of symbol c's slot, byte c & 3 of row c >> 2
-//   rows 64..71  epoch bits : bit 8 of the slot ("accessed since the last renumbering"),
-//                             bit c & 31 of row 64 + (c >> 5)
-//   rows 72..87  slot marks : slot t is some symbol's last access, bit t & 31 of row 72 + (t >> 5)
-//   rows 88..91  word counts: marks in word w, byte w & 3 of row 88 + (w >> 2) (while
-//                             renumbering: marks in the words below w)
-// and, in a VGPR, the marks of each 128-slot superword (byte q of S).
-// 368 B per lane, so six one-wave workgroups fit a CU. Addresses are byte offsets.
-constexpr uint32_t kRowTm = 0, kRowEp = 64, kRowBits = 72, kRowCnt = 88, kRows = 92;
+// Per-lane encode state in LDS, every lane in its own banks (row k of lane l = the dword at byte
+// k * 256 + 4l; the marks are 64-bit rows: word w of lane l = the 8 bytes at kOffMarks + 512w + 8l):
+//   rows 0..63  stamp bytes: the low 8 bits of symbol c's slot, byte c & 3 of row c >> 2
+//   rows 64..71 epoch bits : bit 8 of the slot ("accessed since the last renumbering"),
+//                            bit c & 31 of row 64 + (c >> 5)
+//   marks       512 slot marks as eight 64-bit words: slot t is some symbol's last access
+// and, in a VGPR pair, the number of marks in each 64-slot word (byte w of C). The MTF index of
+// slot t = marks above t in its word (one 64-bit shift, two popcounts) + the counts of the words
+// above (two masked byte sums). 352 B per lane, so seven one-wave workgroups fit a CU; a symbol
+// costs 7 LDS operations (stamp, epoch and marks-word reads; mark clear, new mark, stamp, epoch).
+// (Round 5's layout kept the 32-slot word counts in LDS: 368 B per lane, six workgroups a CU, 10
+// LDS operations a symbol; LDS atomics cost what plain stores cost, tools/microbench/lds_ops.hip.)
+constexpr uint32_t kRowEp = 64, kOffMarks = 72 * 256, kEncLds = kOffMarks + 8 * 512;  // 22528 B per wave
+static_assert(kMtfWgPerCu * kEncLds <= 160 * 1024, "k_mtf_encode: LDS for kMtfWgPerCu workgroups a CU");
 
 __device__ __forceinline__ uint32_t lds_u32(const uint8_t *s, uint32_t a) { return *(const uint32_t *)(s + a); }
+__device__ __forceinline__ uint64_t lds_u64(const uint8_t *s, uint32_t a) { return *(const uint64_t *)(s + a); }
+__device__ __forceinline__ uint32_t a8_of(uint32_t c, uint32_t l4) { return ((c << 6) & 0x3F00u) | l4 | (c & 3u); }
+__device__ __forceinline__ uint32_t ae_of(uint32_t c, uint32_t l4) { return (kRowEp << 8) + (((c >> 5) << 8) | l4); }
+// marks above slot t given t's marks word W and the word counts C; the own mark is counted by the
+// shift and taken off by the accumulator's start value (-1)
+__device__ __forceinline__ uint32_t rank_words(uint64_t C, uint32_t t)
+{
+    const uint64_t M = 0xFFFFFFFFFFFFFF00ull << ((t >> 3) & 0x38u);
+    const uint32_t r = __builtin_amdgcn_sad_u8((uint32_t)C & (uint32_t)M, 0u, 0xFFFFFFFFu);
+    return __builtin_amdgcn_sad_u8((uint32_t)(C >> 32) & (uint32_t)(M >> 32), 0u, r);
+}
+__device__ __forceinline__ uint32_t rank_bits(uint64_t W, uint32_t t, uint32_t acc)
+{
+    const uint64_t ws = W >> (t & 63u);
+    return (uint32_t)__builtin_popcount((uint32_t)(ws >> 32)) + (uint32_t)__builtin_popcount((uint32_t)ws) + acc;
+}
 
-// MTF of symbol c at the wave-uniform slot `now` (the group's first slot now0 is a multiple of
-// 16, k < 16, so all slots of a group share one marks word). Returns the index; the state update
+// MTF of symbol c at the wave-uniform slot `slot` (256..511). Returns the index; the state update
 // (old mark cleared, new mark set, stamp rewritten) happens only for valid symbols.
 template <bool kPred>
-__device__ __forceinline__ uint32_t mtf_step(uint32_t c, bool valid, uint32_t now0, uint32_t k, uint8_t *s, uint32_t l4,
-                                             uint32_t &S)
+__device__ __forceinline__ uint32_t mtf_step(uint32_t c, bool valid, uint32_t slot, uint8_t *s, uint32_t l4, uint32_t l8,
+                                             uint64_t &C)
 {
-    const uint32_t a8 = (kRowTm << 8) + ((c >> 2) << 8) + l4 + (c & 3u);
-    const uint32_t ae = (kRowEp << 8) + ((c >> 5) << 8) + l4;
+    const uint32_t a8 = a8_of(c, l4), ae = ae_of(c, l4);
     const uint32_t lo = s[a8];
     const uint32_t e = lds_u32(s, ae);
     const uint32_t t = lo | (((e >> (c & 31u)) & 1u) << 8);
-    const uint32_t ab = (kRowBits << 8) + ((t >> 5) << 8) + l4;
-    const uint32_t ac = (kRowCnt << 8) + ((t >> 7) << 8) + l4;
-    const uint32_t bw = lds_u32(s, ab), cw = lds_u32(s, ac);
-    const uint32_t sw = (t >> 2) & 24u, ss = (t >> 4) & 24u;
-    uint32_t r = __builtin_popcount((bw >> (t & 31u)) >> 1);
-    r = __builtin_amdgcn_sad_u8(cw & (0xFFFFFF00u << sw), 0u, r);
-    r = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << ss), 0u, r);
+    const uint32_t am = kOffMarks + ((t >> 6) << 9) + l8;
+    const uint64_t W = lds_u64(s, am);
+    const uint32_t r = rank_bits(W, t, rank_words(C, t));
     if (!kPred || valid) {
-        atomicXor((uint32_t *)(s + ab), 1u << (t & 31u));
-        atomicSub((uint32_t *)(s + ac), 1u << sw);
-        S -= 1u << ss;
-        // the new mark: slot now0 + k (uniform word, bit and counters)
-        const uint32_t nw = now0 >> 5;
-        atomicOr((uint32_t *)(s + (kRowBits << 8) + (nw << 8) + l4), 1u << ((now0 & 31u) + k));
-        atomicAdd((uint32_t *)(s + (kRowCnt << 8) + ((nw >> 2) << 8) + l4), 1u << (8 * (nw & 3u)));
-        S += 1u << (8 * (now0 >> 7));
-        s[a8] = (uint8_t)(now0 + k);
+        atomicXor((uint32_t *)(s + am + ((t >> 3) & 4u)), 1u << (t & 31u));
+        C += ~0ull << ((t >> 3) & 0x38u);
+        atomicOr((uint32_t *)(s + kOffMarks + ((slot >> 6) << 9) + l8 + ((slot >> 3) & 4u)), 1u << (slot & 31u));
+        C += 1ull << (8 * (slot >> 6));
+        s[a8] = (uint8_t)slot;
         atomicOr((uint32_t *)(s + ae), 1u << (c & 31u));
     }
     return r;
 }
 
-// A whole super-group (symbols j = 0..63 at slots now + j), software-pipelined: symbol j + 1's
-// stamp and epoch reads are issued before symbol j's state update, and symbol j's marks / counts
-// reads are consumed only after that update has been issued, so each symbol waits on one LDS
-// round trip that overlaps its neighbours' work instead of two back to back. A read-ahead stamp
-// predates the previous symbol's update, so a symbol equal to its predecessor takes the
+// A whole super-group (symbols j = 0..63 at slots now + j; now is a multiple of 64, so the group's
+// new marks fill one 64-bit word), software-pipelined: symbol j + 1's stamp and epoch reads are
+// issued before symbol j's state update, and symbol j's marks word is consumed only one symbol
+// later, so each symbol waits on one LDS round trip that overlaps its neighbours' work. A read-ahead
+// stamp predates the previous symbol's update, so a symbol equal to its predecessor takes the
 // predecessor's slot (the only stamp that update can change). Same results as mtf_step.
-__device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, uint8_t *s, uint32_t l4, uint32_t &S,
-                                          uint4 (&o4)[4])
+__device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, uint8_t *s, uint32_t l4, uint32_t l8,
+                                          uint64_t &C, uint4 (&o4)[4])
 {
     const uint32_t iw[16] = {in[0].x, in[0].y, in[0].z, in[0].w, in[1].x, in[1].y, in[1].z, in[1].w,
                              in[2].x, in[2].y, in[2].z, in[2].w, in[3].x, in[3].y, in[3].z, in[3].w};
     auto sym = [&](int j) { return (iw[j >> 2] >> (8 * (j & 3))) & 255u; };
-    auto a8 = [&](uint32_t c) { return (kRowTm << 8) + ((c >> 2) << 8) + l4 + (c & 3u); };
-    auto ae = [&](uint32_t c) { return (kRowEp << 8) + ((c >> 5) << 8) + l4; };
-    // now is a multiple of 64: the group's marks words are (now >> 5) and the next one, both
-    // counted in one counter row, byte (now >> 5) & 3 (0 or 2) and the byte above
-    const uint32_t bits0 = (kRowBits << 8) + ((now >> 5) << 8) + l4;
-    const uint32_t cnt0 = (kRowCnt << 8) + ((now >> 7) << 8) + l4;
-    const uint32_t inc0 = 1u << (8 * ((now >> 5) & 3u)), sinc = 1u << (8 * (now >> 7));
+    const uint32_t amn = kOffMarks + ((now >> 6) << 9) + l8;  // the group's marks word
+    const uint64_t cinc = 1ull << (8 * (now >> 6));
     uint32_t ow[16];
     uint32_t plo[64], pe[64];  // read-ahead stamp bytes / epoch words (registers once unrolled)
-#pragma unroll
-    for (int j = 0; j < kMtfAhead; ++j) {
-        plo[j] = s[a8(sym(j))];
-        pe[j] = lds_u32(s, ae(sym(j)));
-    }
-    uint32_t pbw = 0, pcw = 0, pt = 0, psw = 0, pr = 0;  // the previous symbol's deferred rank terms
+    plo[0] = s[a8_of(sym(0), l4)];
+    pe[0] = lds_u32(s, ae_of(sym(0), l4));
+    uint64_t pW = 0;
+    uint32_t pt = 0, pr = 0;  // the previous symbol's marks word, slot and word-count term
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
         const uint32_t c = sym(j);
-        if (j + kMtfAhead < 64) {
-            const uint32_t cn = sym(j + kMtfAhead);
-            plo[j + kMtfAhead] = s[a8(cn)];
-            pe[j + kMtfAhead] = lds_u32(s, ae(cn));
+        if (j + 1 < 64) {
+            const uint32_t cn = sym(j + 1);
+            plo[j + 1] = s[a8_of(cn, l4)];
+            pe[j + 1] = lds_u32(s, ae_of(cn, l4));
         }
         uint32_t t = plo[j] | (((pe[j] >> (c & 31u)) & 1u) << 8);
-#pragma unroll
-        for (int d = kMtfAhead; d >= 1; --d)  // updates the read-ahead missed, the nearest last
-            if (j >= d) t = c == sym(j - d) ? now + (uint32_t)(j - d) : t;
-        const uint32_t ab = (kRowBits << 8) + ((t >> 5) << 8) + l4;
-        const uint32_t ac = (kRowCnt << 8) + ((t >> 7) << 8) + l4;
-        const uint32_t bw = lds_u32(s, ab), cw = lds_u32(s, ac);
-        const uint32_t sw = (t >> 2) & 24u, ss = (t >> 4) & 24u;
-        const uint32_t rs = __builtin_amdgcn_sad_u8(S & (0xFFFFFF00u << ss), 0u, 0u);
-        atomicXor((uint32_t *)(s + ab), 1u << (t & 31u));
-        atomicSub((uint32_t *)(s + ac), 1u << sw);
-        S -= 1u << ss;
-        // the new mark, slot now + j: word (now >> 5) + (j >> 5), counter byte of that word
-        atomicOr((uint32_t *)(s + bits0 + ((j >> 5) << 8)), 1u << (j & 31));
-        atomicAdd((uint32_t *)(s + cnt0), j < 32 ? inc0 : inc0 << 8);
-        S += sinc;
-        s[a8(c)] = (uint8_t)(now + (uint32_t)j);
-        atomicOr((uint32_t *)(s + ae(c)), 1u << (c & 31u));
+        if (j >= 1) t = c == sym(j - 1) ? now + (uint32_t)(j - 1) : t;
+        const uint32_t am = kOffMarks + ((t >> 6) << 9) + l8;
+        const uint64_t W = lds_u64(s, am);
+        const uint32_t rw = rank_words(C, t);
+        atomicXor((uint32_t *)(s + am + ((t >> 3) & 4u)), 1u << (t & 31u));
+        C += ~0ull << ((t >> 3) & 0x38u);
+        atomicOr((uint32_t *)(s + amn + 4 * (j >> 5)), 1u << (j & 31));
+        C += cinc;
+        s[a8_of(c, l4)] = (uint8_t)(now + (uint32_t)j);
+        atomicOr((uint32_t *)(s + ae_of(c, l4)), 1u << (c & 31u));
         __builtin_amdgcn_sched_barrier(0);
         if (j > 0) {
-            uint32_t r = __builtin_amdgcn_sad_u8(pcw & (0xFFFFFF00u << psw), 0u,
-                                                 __builtin_popcount((pbw >> (pt & 31u)) >> 1) + pr);
+            uint32_t r = rank_bits(pW, pt, pr);
             asm volatile("" : "+v"(r));  // computed here, not sunk to the stores (64 symbols' terms live)
             const int q = j - 1;
             ow[q >> 2] = (q & 3) ? ow[q >> 2] | (r << (8 * (q & 3))) : r;
         }
-        pbw = bw;
-        pcw = cw;
+        pW = W;
         pt = t;
-        psw = sw;
-        pr = rs;
+        pr = rw;
     }
-    const uint32_t r = __builtin_amdgcn_sad_u8(pcw & (0xFFFFFF00u << psw), 0u,
-                                               __builtin_popcount((pbw >> (pt & 31u)) >> 1) + pr);
-    ow[15] |= r << 24;
+    ow[15] |= rank_bits(pW, pt, pr) << 24;
 #pragma unroll
     for (int q = 0; q < 4; ++q) o4[q] = make_uint4(ow[4 * q], ow[4 * q + 1], ow[4 * q + 2], ow[4 * q + 3]);
 }
 
 // Slots 0..255 marked (the start alphabet or the renumbered window), epochs cleared.
-__device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t &S)
+__device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t l8, uint64_t &C)
 {
 #pragma unroll
-    for (uint32_t w = 0; w < 16; ++w) *(uint32_t *)(s + ((kRowBits + w) << 8) + l4) = w < 8 ? 0xffffffffu : 0u;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) *(uint32_t *)(s + ((kRowCnt + q) << 8) + l4) = q < 2 ? 0x20202020u : 0u;
+    for (uint32_t w = 0; w < 8; ++w) *(uint64_t *)(s + kOffMarks + (w << 9) + l8) = w < 4 ? ~0ull : 0ull;
 #pragma unroll
     for (uint32_t w = 0; w < 8; ++w) *(uint32_t *)(s + ((kRowEp + w) << 8) + l4) = 0u;
-    S = 0x00008080u;
+    C = 0x0000000040404040ull;
 }
 
-// The window is full (slot 512 reached): every symbol's new slot is the number of marks below
-// its slot (0..255, order kept). The word-count rows are overwritten with the marks below each
-// word first, so a symbol costs two LDS reads and a masked popcount.
-__device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_t &S)
+// The window is full (slot 512 reached): every symbol's new slot is the number of marks below its
+// slot (0..255, order kept): the marks in the words below (byte prefix sums of C; a byte only
+// overflows past the last marked word, which no symbol reads) + the marks below it in its word.
+__device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_t l8, uint64_t &C)
 {
-    uint32_t run = 0, pw[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (uint32_t w = 0; w < 16; ++w) {
-        pw[w >> 2] |= (run & 255u) << (8 * (w & 3u));  // only words holding a mark are read
-        run += __builtin_popcount(lds_u32(s, ((kRowBits + w) << 8) + l4));
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) *(uint32_t *)(s + ((kRowCnt + q) << 8) + l4) = pw[q];
+    uint64_t P = C << 8;
+    P += P << 8;
+    P += P << 16;
+    P += P << 32;
 #pragma nounroll
     for (uint32_t w = 0; w < 8; ++w) {  // symbols 32w .. 32w + 31
         const uint32_t e = lds_u32(s, ((kRowEp + w) << 8) + l4);
@@ -440,14 +423,16 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
             for (uint32_t b = 0; b < 4; ++b) {
                 const uint32_t k = 4 * j + b;
                 const uint32_t t = ((tw[j] >> (8 * b)) & 255u) | (((e >> k) & 1u) << 8);
-                const uint32_t below = s[(kRowCnt << 8) + ((t >> 7) << 8) + l4 + ((t >> 5) & 3u)];
-                const uint32_t bw = lds_u32(s, (kRowBits << 8) + ((t >> 5) << 8) + l4);
-                nwd |= (below + __builtin_popcount(bw & ((1u << (t & 31u)) - 1u))) << (8 * b);
+                const uint64_t W = lds_u64(s, kOffMarks + ((t >> 6) << 9) + l8);
+                const uint64_t below = W & ((1ull << (t & 63u)) - 1u);
+                const uint32_t nb = (uint32_t)(P >> ((t >> 3) & 0x38u)) & 255u;
+                nwd |= ((uint32_t)__builtin_popcount((uint32_t)(below >> 32)) + (uint32_t)__builtin_popcount((uint32_t)below) + nb)
+                       << (8 * b);
             }
             *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = nwd;
         }
     }
-    window_reset(s, l4, S);
+    window_reset(s, l4, l8, C);
 }
 
 // grid = ceil(chunks / 64); one lane per chunk. Chunks start 64-byte aligned except a block's
@@ -461,9 +446,9 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
                                                        uint32_t nch, const uint32_t *__restrict__ Sst,
                                                        uint8_t *__restrict__ out)
 {
-    __shared__ uint32_t st32[kRows * kLanes];
-    uint8_t *s = (uint8_t *)st32;
-    const uint32_t l = threadIdx.x, l4 = 4 * l;
+    __shared__ uint64_t st64[kEncLds / 8];
+    uint8_t *s = (uint8_t *)st64;
+    const uint32_t l = threadIdx.x, l4 = 4 * l, l8 = 8 * l;
     const uint32_t g = blockIdx.x * kLanes + l;
     const bool live = g < nch;
     const MChunk ch = live ? chunks[g] : MChunk{0, 0, 0, 0};
@@ -474,12 +459,13 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
 #pragma unroll
             for (uint32_t j = 0; j < 4; ++j) {
                 const uint32_t c = (w >> (8 * j)) & 255u;
-                s[((c >> 2) << 8) + l4 + (c & 3u)] = (uint8_t)(255 - (4 * k4 + j));
+                s[a8_of(c, l4)] = (uint8_t)(255 - (4 * k4 + j));
             }
         }
     }
-    uint32_t S, now = 256;
-    window_reset(s, l4, S);
+    uint64_t C;
+    uint32_t now = 256;
+    window_reset(s, l4, l8, C);
     const uint32_t base = ch.start & ~63u, end = ch.start + ch.len;
     const uint32_t nsg = live ? (((end + 63u) & ~63u) - base) >> 6 : 0u;
     auto whole = [&](uint32_t gi) {
@@ -506,7 +492,7 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         load_sg(sg + 1, pf);
         if (whole(sg)) {
             uint4 o4[4];
-            mtf_whole(in, now, s, l4, S, o4);
+            mtf_whole(in, now, s, l4, l8, C, o4);
             uint4 *po = (uint4 *)(out + a0);
 #pragma unroll
             for (int q = 0; q < 4; ++q) po[q] = o4[q];
@@ -522,7 +508,7 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
                 for (uint32_t k = 0; k < 16; ++k) {
                     const uint32_t c = (iw[k >> 2] >> (8 * (k & 3))) & 255u;
                     const bool v = a + k >= ch.start && a + k < end;
-                    o[k >> 2] |= (mtf_step<true>(c, v, now + 16 * q, k, s, l4, S) & 255u) << (8 * (k & 3));
+                    o[k >> 2] |= (mtf_step<true>(c, v, now + 16 * q + k, s, l4, l8, C) & 255u) << (8 * (k & 3));
                 }
                 for (uint32_t k = 0; k < 16; ++k)
                     if (a + k >= ch.start && a + k < end) out[a + k] = (uint8_t)(o[k >> 2] >> (8 * (k & 3)));
@@ -530,7 +516,7 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
         }
         now += 64;  // 256 + 64 per super-group: the window fills up exactly at a boundary
         if (now == 512) {
-            window_renumber(s, l4, S);
+            window_renumber(s, l4, l8, C);
             now = 256;
         }
     }
