@@ -82,6 +82,8 @@ _SIGS = {
     "bmh_compress_host": (C.c_int, [P, P, U64, U64, P, U64, PU64]),
     "bmh_compress_host_multi": (C.c_int, [C.POINTER(P), U32, P, U64, U64, P, U64, PU64]),
     "bmh_compress_bound": (U64, [U64, U64]),
+    "bmh_host_cpus": (U32, []),
+    "bmh_copy_threads": (U32, [U32, U32]),
     "bmh_decompress_host": (C.c_int, [P, U64, P, U64, PU64]),
     "bmh_record_to_mtf": (C.c_int, [P, U64, P, U64, PU64]),
     "bmh_decode_blocks_dev": (C.c_int, [P, P, PU64, U32, P, U64, PU64]),
@@ -107,7 +109,10 @@ def lib() -> C.CDLL:
             raise BmhError(BMH_ENODEV, f"libbmh.so not built at {LIB_PATH} (run __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            f = getattr(L, name)
+            try:
+                f = getattr(L, name)
+            except AttributeError:  # an older library under BMH_LIB (A/B runs); the export test checks ours
+                continue
             f.restype = res
             f.argtypes = args
         _lib = L
@@ -254,7 +259,7 @@ class Context:
         return int(lib().bmh_ctx_spec_fallbacks(self.h))
 
     # ---- tuning options (include/bmh.h BMH_OPT_*; 0 restores the library's rule)
-    OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5}
+    OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5, "one_pipeline": 6}
 
     def set_option(self, name: str, value: int) -> None:
         _check(lib().bmh_ctx_set_option(self.h, self.OPTIONS[name], int(value)), f"set_option({name})")

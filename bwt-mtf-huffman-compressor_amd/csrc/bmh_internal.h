@@ -98,7 +98,7 @@ struct Ctx {
     // tuning options (bmh_ctx_set_option; 0 = the library's rule); sub-pipelines and the side
     // context copy their parent's at every call
     struct Options {
-        uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0;
+        uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0, one_pipeline = 0;
     } opt;
     uint32_t last_pipelines = 0;  // pipelines of the last device batch encode (encode_blocks)
     uint64_t zipf_resume_tok0 = 0, zipf_resume_base = 0;  // synth_zipf: start of its last round
@@ -122,6 +122,8 @@ struct Ctx {
     void *dbl_cnt_host = nullptr;  // rank doubling: two rounds' counters (pinned), read one round late
     hipEvent_t dbl_ev[2] = {};
     uint64_t pre_sig = 0;  // bwt_batch_core's prologue already launched for this input + layout
+    uint32_t copy_share = 1;  // contexts streaming host buffers at once (bmh_compress_host_multi)
+    uint64_t dense_sig = 0;  // layout of the last batch dense_batch found dense (prologue queued early)
     bool spec_lists = false, spec_pending = false;
     bool mtf_dense = false;  // the batch was found dense: MTF stages skip their run-aware paths
     std::vector<uint64_t> roffs_host;  // encode_blocks_one: record offsets + status, one copy

@@ -711,9 +711,20 @@ bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt)
     BMH_HIP(hipEventRecord(c->probe_ev, c->stream));
     // a batch past the run screen that turns out dense runs bwt_batch_core on this context and
     // stream: its global-pass prologue is queued behind the census now, so the GPU works through
-    // the host's wait and the launches that follow it (a batch kept on several pipelines leaves
-    // it unused: ~0.1 ms of one stream)
-    if (bt.total > kRunScreenMax && !c->opt.pipelines) bwt_batch_core(c, d_in, bt, nullptr, nullptr, true);
+    // the host's wait and the launches that follow it. Only when the last batch of this layout was
+    // dense: the prologue sizes every BWT workspace of this context (~40 B per input byte), which a
+    // text batch, encoded on the sub-pipelines' own contexts, would leave allocated here unused
+    // (ADVICE r5). A prologue that cannot allocate is skipped (pre_sig stays unset; the batch then
+    // runs its own prologue).
+    const uint64_t lsig = layout_sig(11, bt.offs, 0);
+    if (bt.total > kRunScreenMax && !c->opt.pipelines && c->dense_sig == lsig) {
+        try {
+            bwt_batch_core(c, d_in, bt, nullptr, nullptr, true);
+        } catch (const Error &e) {
+            if (e.status != BMH_ENOMEM) throw;
+            c->pre_sig = 0;
+        }
+    }
     for (;;) {  // spin: a blocking wait can sleep the host thread for milliseconds
         const hipError_t e = hipEventQuery(c->probe_ev);
         if (e == hipSuccess) break;
@@ -725,7 +736,9 @@ bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt)
         const uint64_t m = std::min<uint64_t>(n, kProbeSample);
         if (m >= 4096 && 2ull * c->probe_host[b] >= m) dense += n;
     }
-    return dense * 10 >= bt.total * 9;
+    const bool is_dense = dense * 10 >= bt.total * 9;
+    c->dense_sig = is_dense ? lsig : 0;
+    return is_dense;
 }
 
 // Batch BWT: small batches are screened for run-heavy blocks, which take the run path above;

@@ -16,6 +16,8 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <sched.h>
+#include <cstring>
 
 namespace bmh {
 
@@ -168,9 +170,25 @@ Batch make_batch(const uint64_t *offs, uint32_t nblocks)
 
 uint64_t record_bound(uint64_t n) { return kRecordHeader + 320 + n + 16; }
 
-// Device batch encode -> records at d_out; fills rec_offs (nblocks + 1).
+static void encode_blocks_one_(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
+                               uint64_t *rec_offs, OffsetChain *chain, int sub, bool spec);
+
+// Device batch encode -> records at d_out; fills rec_offs (nblocks + 1). An exception can leave a
+// status bit set on the device (k_huff_build sets it before the read-back): the status tag is
+// cleared then, so the next batch of the same layout zeroes the word again.
 static void encode_blocks_one(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
                               uint64_t *rec_offs, OffsetChain *chain, int sub, bool spec = false)
+{
+    try {
+        encode_blocks_one_(c, d_in, bt, d_out, out_cap, rec_offs, chain, sub, spec);
+    } catch (...) {
+        c->ws_tag[WS_STATUS] = 0;
+        throw;
+    }
+}
+
+static void encode_blocks_one_(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out, uint64_t out_cap,
+                               uint64_t *rec_offs, OffsetChain *chain, int sub, bool spec)
 {
     // BWT -> MTF (+ histograms) -> code books, record offsets and headers -> bit pack, all
     // on the context stream; the host waits on the BWT's list counters, and once at the end
@@ -349,6 +367,7 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
         spec = true;
     }
     c->pre_sig = spec ? c->pre_sig : 0;  // a prologue dense_batch launched for one pipeline, unused
+    if (c->opt.one_pipeline) S = 1;       // (a timing pass: the decisions above stand)
     c->last_pipelines = (uint32_t)std::max(S, 1);
     if (S <= 1) {
         encode_blocks_one(c, d_in, bt, d_out, out_cap, rec_offs, nullptr, 0, spec);
@@ -460,11 +479,52 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, uint64_t bytes, unsigne
     for (auto &x : th) x.join();
 }
 
-static unsigned copy_threads()
+// CPUs this process may run on: its affinity set, capped by the cgroup CPU quota (cgroup v2
+// cpu.max, else v1 cfs_quota_us / cfs_period_us, rounded up). hardware_concurrency() reports the
+// whole machine: 256 on the driver's boxes, whose cgroup grants 16 (bench.py's cpu_baseline
+// learned the same: 256 processes under that quota ran at 59 MB/s against 96 with 16).
+static unsigned read_quota_cpus()
 {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    return std::min(16u, hw);
+    long long q = -1, per = -1;
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char a[32] = {0};
+        if (fscanf(f, "%31s %lld", a, &per) == 2 && strcmp(a, "max") != 0) q = atoll(a);
+        fclose(f);
+    } else if (FILE *g = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        if (fscanf(g, "%lld", &q) != 1) q = -1;
+        fclose(g);
+        if (FILE *h = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (fscanf(h, "%lld", &per) != 1) per = -1;
+            fclose(h);
+        }
+    }
+    if (q <= 0 || per <= 0) return 0;  // no quota
+    return (unsigned)std::max<long long>(1, (q + per - 1) / per);
 }
+
+static unsigned host_cpus()
+{
+    static const unsigned v = [] {
+        unsigned n = 0;
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) n = (unsigned)CPU_COUNT(&set);
+        if (n == 0) n = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned q = read_quota_cpus();
+        return q ? std::min(n, q) : n;
+    }();
+    return v;
+}
+
+// Copy threads per copy site (the loader's pageable -> pinned staging copies and the writer's
+// record copies run side by side): the process's CPUs divided among the contexts that stream at
+// once (bmh_compress_host_multi sets Ctx::copy_share), at most 16 and at least 1. Before round 6
+// every context sized its copies from hardware_concurrency(): 8 contexts started up to 128 copy
+// threads a site on a box granting 16 CPUs.
+static unsigned copy_threads_for(unsigned cpus, unsigned share)
+{
+    return std::max(1u, std::min(16u, cpus / std::max(1u, share)));
+}
+static unsigned copy_threads(const Ctx *c = nullptr) { return copy_threads_for(host_cpus(), c ? c->copy_share : 1u); }
 
 // Page-locked (hipHostMalloc'd or hipHostRegister'ed) host range that device `dev`'s DMA engines
 // may read and write directly, so the streaming encoder skips its staging copies. The range is
@@ -589,7 +649,7 @@ static void encode_host_blocks(Ctx *c, const uint8_t *in, uint64_t n, uint64_t b
         BMH_HIP(hipEventCreateWithFlags(&ev_h2d[s], hipEventDisableTiming));
         BMH_HIP(hipEventCreateWithFlags(&ev_d2h[s], hipEventDisableTiming));
     }
-    const unsigned nt = copy_threads();
+    const unsigned nt = copy_threads(c);
     std::mutex m;
     std::condition_variable cv;
     size_t loaded = 0;    // batches whose H2D is issued
@@ -1030,6 +1090,8 @@ uint32_t bmh_encode_pipelines(bmh_ctx *c, uint64_t total, uint32_t nblocks)
 }
 
 uint32_t bmh_ctx_last_pipelines(bmh_ctx *c) { return c ? c->last_pipelines : 0u; }
+uint32_t bmh_host_cpus(void) { return host_cpus(); }
+uint32_t bmh_copy_threads(uint32_t nctx, uint32_t cpus) { return copy_threads_for(cpus ? cpus : host_cpus(), nctx); }
 uint32_t bmh_ctx_spec_fallbacks(bmh_ctx *c) { return c ? c->spec_fallbacks : 0u; }
 
 uint64_t bmh_payload_bytes(const bmh_code_table *t, const uint64_t freq[256])
@@ -1106,8 +1168,14 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
     uint64_t at = table;
     if (direct && table > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
     std::vector<bmh_status> st(nctx, BMH_OK);
+    struct Share {  // the contexts streaming at once split the host's copy threads
+        Ctx *c;
+        Share(Ctx *x, uint32_t n) : c(x) { c->copy_share = n; }
+        ~Share() { c->copy_share = 1; }
+    };
     auto work = [&](uint32_t g) {
         try {
+            Share share(ctxs[g], nctx);
             use_device(ctxs[g]);
             std::vector<uint64_t> bl;
             for (uint64_t b = g; b < nblocks; b += nctx) bl.push_back(b);
@@ -1118,7 +1186,7 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
                     [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
                         const uint64_t bytes = ro[cnt];
                         if (at + bytes > out_cap) fail(BMH_ERANGE, "compress: output capacity too small");
-                        if (src != out + at) par_memcpy(out + at, src, bytes, copy_threads());
+                        if (src != out + at) par_memcpy(out + at, src, bytes, copy_threads(ctxs[g]));
                         for (size_t i = 0; i < cnt; ++i) {
                             if (table) put_u64(out + 32 + 8 * (i0 + i), ro[i + 1] - ro[i]);
                         }
@@ -1130,7 +1198,7 @@ bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t 
                                    [&](size_t i0, size_t cnt, const uint8_t *src, const uint64_t *ro) {
                                        const uint64_t bytes = ro[cnt];
                                        std::unique_ptr<uint8_t[]> buf(new uint8_t[std::max<uint64_t>(bytes, 1)]);
-                                       par_memcpy(buf.get(), src, bytes, copy_threads());
+                                       par_memcpy(buf.get(), src, bytes, copy_threads(ctxs[g]));
                                        for (size_t i = 0; i < cnt; ++i)
                                            recs[bl[i0 + i]] = RecRef{buf.get() + ro[i], ro[i + 1] - ro[i]};
                                        store[g].push_back(std::move(buf));
@@ -1291,6 +1359,7 @@ bmh_status bmh_ctx_set_option(bmh_ctx *c, uint32_t option, uint64_t value)
         c->opt.mtf_chunk = value;
         break;
     case BMH_OPT_CHECK_LISTS: c->opt.check_lists = value != 0; break;
+    case BMH_OPT_ONE_PIPELINE: c->opt.one_pipeline = value != 0; break;
     default: fail(BMH_EINVAL, "set_option: unknown option " + std::to_string(option));
     }
     API_END

@@ -2,7 +2,7 @@
 // (main.cpp:415-457) whose three compile-time modes become subcommands:
 //
 //   bmh compress   <in> <out> [--block-size N] [--gpus G]   (-DCOMPRESS,      main.cpp:439-447)
-//   bmh decompress <in> <out>                               (-DDECOMPRESS,    main.cpp:448-456)
+//   bmh decompress <in> <out> [--host]                      (-DDECOMPRESS,    main.cpp:448-456)
 //   bmh full_pipeline [dir]                                 (-DFULL_PIPELINE, main.cpp:416-438)
 //
 // Invoked through a link named bmh_compress / bmh_decompress / bmh_full_pipeline it takes the
@@ -111,18 +111,24 @@ int do_compress(Gpus &g, const std::string &in, const std::string &outn, uint64_
     return 0;
 }
 
-int do_decompress(const std::string &in, const std::string &outn)
+// decompress(): main.cpp:327-345, decoded on the GPU (bmh_decompress_dev on the first context);
+// with no context (`--host`) by libbmh's host C++ decoder
+int do_decompress(bmh_ctx *ctx, const std::string &in, const std::string &outn)
 {
     std::vector<uint8_t> data;
     if (!read_file(in, data)) {
         std::cerr << "bmh: cannot read " << in << std::endl;
         return 2;
     }
+    auto dec = [&](uint8_t *out, uint64_t cap, uint64_t *n) {
+        return ctx ? bmh_decompress_dev(ctx, data.data(), data.size(), out, cap, n)
+                   : bmh_decompress_host(data.data(), data.size(), out, cap, n);
+    };
     uint64_t n = 0;
-    int st = bmh_decompress_host(data.data(), data.size(), nullptr, 0, &n);
+    int st = dec(nullptr, 0, &n);
     if (st != BMH_OK) return die("decompress", st);
     std::vector<uint8_t> out(n);
-    st = bmh_decompress_host(data.data(), data.size(), out.data(), n, &n);
+    st = dec(out.data(), n, &n);
     if (st != BMH_OK) return die("decompress", st);
     if (!write_file(outn, out.data(), n)) {
         std::cerr << "bmh: cannot write " << outn << std::endl;
@@ -148,7 +154,7 @@ int do_full_pipeline(Gpus &g, std::string dir)
         std::cout << k++ << "/" << 14 << ' ';
         const std::string in = dir + f, enc = dir + f + ".bzap", dec = dir + f + ".decoded";
         int rc = do_compress(g, in, enc, 0);
-        if (rc == 0) rc = do_decompress(enc, dec);
+        if (rc == 0) rc = do_decompress(g.ctx[0], enc, dec);
         const bool ok = rc == 0 && same_file(in, dec);
         bad += !ok;
         std::cout << (ok ? "success" : "fail") << std::endl;
@@ -159,7 +165,7 @@ int do_full_pipeline(Gpus &g, std::string dir)
 int usage()
 {
     std::cerr << "usage: bmh compress <in> <out> [--block-size N] [--gpus G]\n"
-                 "       bmh decompress <in> <out>\n"
+                 "       bmh decompress <in> <out> [--host]   (--host: the host C++ decoder instead of the GPU)\n"
                  "       bmh full_pipeline [calgarycorpus_dir]\n";
     return 1;
 }
@@ -183,10 +189,12 @@ int main(int argc, char **argv)
     }
     uint64_t bs = 0;
     int gpus = 1;
+    bool host = false;
     std::vector<std::string> pos;
     for (size_t i = 0; i < args.size(); ++i) {
         if (args[i] == "--block-size" && i + 1 < args.size()) bs = std::stoull(args[++i]);
         else if (args[i] == "--gpus" && i + 1 < args.size()) gpus = std::stoi(args[++i]);
+        else if (args[i] == "--host") host = true;
         else pos.push_back(args[i]);
     }
     if (mode == "compress" || mode == "decompress") {
@@ -194,10 +202,11 @@ int main(int argc, char **argv)
             std::cout << "Wrong arguments. Pass only input and output file as parameters";
             return 1;
         }
-        if (mode == "decompress") return do_decompress(pos[0], pos[1]);
+        if (mode == "decompress" && host) return do_decompress(nullptr, pos[0], pos[1]);
         Gpus g;
         int st = g.open(gpus);
         if (st != BMH_OK) return die("gpu", st);
+        if (mode == "decompress") return do_decompress(g.ctx[0], pos[0], pos[1]);
         return do_compress(g, pos[0], pos[1], bs);
     }
     if (mode == "full_pipeline") {

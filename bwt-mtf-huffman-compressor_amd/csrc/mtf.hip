@@ -356,6 +356,7 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
     pe[0] = lds_u32(s, ae_of(sym(0), l4));
     uint64_t pW = 0;
     uint32_t pt = 0, pr = 0;  // the previous symbol's marks word, slot and word-count term
+    uint32_t slot = now, pslot = now;  // this / the previous symbol's slot, in a VGPR (stamp data and forward)
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
         const uint32_t c = sym(j);
@@ -364,8 +365,8 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
             plo[j + 1] = s[a8_of(cn, l4)];
             pe[j + 1] = lds_u32(s, ae_of(cn, l4));
         }
-        uint32_t t = plo[j] | (((pe[j] >> (c & 31u)) & 1u) << 8);
-        if (j >= 1) t = c == sym(j - 1) ? now + (uint32_t)(j - 1) : t;
+        uint32_t t = plo[j] | (__builtin_amdgcn_ubfe(pe[j], c & 31u, 1u) << 8);
+        if (j >= 1) t = c == sym(j - 1) ? pslot : t;
         const uint32_t am = kOffMarks + ((t >> 6) << 9) + l8;
         const uint64_t W = lds_u64(s, am);
         const uint32_t rw = rank_words(C, t);
@@ -373,7 +374,7 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
         C += ~0ull << ((t >> 3) & 0x38u);
         atomicOr((uint32_t *)(s + amn + 4 * (j >> 5)), 1u << (j & 31));
         C += cinc;
-        s[a8_of(c, l4)] = (uint8_t)(now + (uint32_t)j);
+        s[a8_of(c, l4)] = (uint8_t)slot;
         atomicOr((uint32_t *)(s + ae_of(c, l4)), 1u << (c & 31u));
         __builtin_amdgcn_sched_barrier(0);
         if (j > 0) {
@@ -385,6 +386,9 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
         pW = W;
         pt = t;
         pr = rw;
+        pslot = slot;
+        slot += 1;
+        asm volatile("" : "+v"(slot));
     }
     ow[15] |= rank_bits(pW, pt, pr) << 24;
 #pragma unroll
@@ -410,6 +414,7 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
     P += P << 8;
     P += P << 16;
     P += P << 32;
+#ifndef BMH_PROBE_NORENUM  // timing probe: renumbering skipped (wrong output)
 #pragma nounroll
     for (uint32_t w = 0; w < 8; ++w) {  // symbols 32w .. 32w + 31
         const uint32_t e = lds_u32(s, ((kRowEp + w) << 8) + l4);
@@ -432,6 +437,7 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
             *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = nwd;
         }
     }
+#endif
     window_reset(s, l4, l8, C);
 }
 

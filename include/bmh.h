@@ -150,6 +150,11 @@ bmh_status bmh_compress_host(bmh_ctx *ctx, const uint8_t *in, uint64_t n, uint64
 bmh_status bmh_compress_host_multi(bmh_ctx **ctxs, uint32_t nctx, const uint8_t *in, uint64_t n,
                                    uint64_t block_size, uint8_t *out, uint64_t out_cap, uint64_t *out_len);
 uint64_t bmh_compress_bound(uint64_t n, uint64_t block_size);
+/* CPUs this process may use: its affinity set capped by the cgroup CPU quota. */
+uint32_t bmh_host_cpus(void);
+/* Copy threads per copy site each of nctx contexts streaming at once uses for its pageable <->
+ * page-locked staging copies (cpus 0: bmh_host_cpus()): cpus / nctx, clamped to [1, 16]. */
+uint32_t bmh_copy_threads(uint32_t nctx, uint32_t cpus);
 
 /* ---- decode (host C++; replaces decompress(), main.cpp:327-345) -------------------- */
 /* Decodes one reference record or one BMH container. *n_out receives the decoded size;
@@ -186,7 +191,10 @@ enum {
     BMH_OPT_STREAM_BATCH = 2, /* bmh_compress_host batch bytes (default 256 MiB) */
     BMH_OPT_MAX_BATCH = 3,    /* largest device batch bytes of the host-buffer paths (default 1 GiB) */
     BMH_OPT_MTF_CHUNK = 4,    /* MTF chunk symbols, 64..4096 (default: adaptive) */
-    BMH_OPT_CHECK_LISTS = 5   /* 1: check every BWT list round and print its census (diagnostic, slow) */
+    BMH_OPT_CHECK_LISTS = 5,  /* 1: check every BWT list round and print its census (diagnostic, slow) */
+    BMH_OPT_ONE_PIPELINE = 6  /* 1: run each device batch on one pipeline AFTER the library's own
+                               * decisions (the dense-batch census and its speculative list round
+                               * still apply), so a one-stream timing pass runs the default path */
 };
 bmh_status bmh_ctx_set_option(bmh_ctx *ctx, uint32_t option, uint64_t value);
 

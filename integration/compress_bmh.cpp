@@ -56,13 +56,14 @@ void compress(const std::string &initial_file_name, const std::string &encoded_f
 void decompress(const std::string &encoded_file_name, const std::string &decoded_file_name)
 {
     const auto &[record, dummy1, dummy2, dummy3] = read_bytes(encoded_file_name);
-    // bytes_to_tree -> huffman_reverse -> move_to_front_reverse -> bwt_reverse (main.cpp:331-342);
-    // bmh_decompress_host is libbmh's host decoder (bmh_decompress_dev decodes on the GPU)
+    // bytes_to_tree -> huffman_reverse -> move_to_front_reverse -> bwt_reverse (main.cpp:331-342)
+    // on the GPU (bmh_decompress_dev: record H2D, the decode kernels, the block D2H); the first
+    // call (out = NULL) reads only the size from the header
     uint64_t n = 0;
-    if (bmh_decompress_host(record.data(), record.size(), nullptr, 0, &n) != BMH_OK)
+    if (bmh_decompress_dev(bmh_context(), record.data(), record.size(), nullptr, 0, &n) != BMH_OK)
         throw std::runtime_error(bmh_last_error());
     std::vector<unsigned char> decoded_data(n);
-    if (bmh_decompress_host(record.data(), record.size(), decoded_data.data(), n, &n) != BMH_OK)
+    if (bmh_decompress_dev(bmh_context(), record.data(), record.size(), decoded_data.data(), n, &n) != BMH_OK)
         throw std::runtime_error(bmh_last_error());
     write_bytes(decoded_file_name, decoded_data);
 }

@@ -906,7 +906,7 @@ def test_tuning_options_never_change_records(ctx, oracle):
     for i in (0, 6, 12, 15):  # the default's short MTF chunks take the five-level composition
         assert want[i] == oracle.encode(blocks[i]), i
     try:
-        for name, vals in (("pipelines", (1, 2, 3, 4, 5)), ("mtf_chunk", (64, 1024, 4096)), ("check_lists", (1,))):
+        for name, vals in (("pipelines", (1, 2, 3, 4, 5)), ("mtf_chunk", (64, 1024, 4096)), ("check_lists", (1,)), ("one_pipeline", (1,))):
             for v in vals:
                 ctx.set_option(name, v)
                 assert ctx.encode_blocks(blocks) == want, (name, v)

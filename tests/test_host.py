@@ -134,12 +134,16 @@ def test_cli_host_modes(tmp_path):
     src = tmp_path / "bib.bzap"
     src.write_bytes(rec)
     out = tmp_path / "bib.out"
-    r = subprocess.run([CLI, "decompress", str(src), str(out)], capture_output=True, text=True)
+    # --host: libbmh's host C++ decoder (bmh decompress decodes on the GPU by default)
+    r = subprocess.run([CLI, "decompress", str(src), str(out), "--host"], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert out.read_bytes() == data
     if bmh.lib().bmh_device_count() == 0:
         r = subprocess.run([CLI, "compress", str(out), str(tmp_path / "x.bzap")], capture_output=True, text=True)
         assert r.returncode != 0 and "device" in (r.stderr + r.stdout).lower()
+        r = subprocess.run([CLI, "decompress", str(src), str(tmp_path / "y.out")], capture_output=True, text=True)
+        assert r.returncode != 0 and "device" in (r.stderr + r.stdout).lower()
+        assert not (tmp_path / "y.out").exists()
 
 
 @pytest.mark.parametrize("nsym", [2, 12, 34, 38, 60])
@@ -202,3 +206,40 @@ def test_compress_host_multi_rejects_bad_context_lists():
                                        olen.ctypes.data_as(bmh.PU64))
         assert st == bmh.BMH_EINVAL
         assert "context" in L.bmh_last_error().decode()
+
+
+def _cgroup_cpus():
+    """The CPU count this process may use, restated: affinity set, capped by the cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    q = None
+    try:
+        a, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if a != "max":
+            q = -(-int(a) // int(per))
+    except (OSError, ValueError):
+        try:
+            qa = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            pe = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if qa > 0 and pe > 0:
+                q = -(-qa // pe)
+        except (OSError, ValueError):
+            q = None
+    return max(1, min(n, q)) if q else n
+
+
+def test_copy_thread_budget_follows_cpus_and_contexts():
+    """the host-buffer path's staging copies are sized from the CPUs the process
+    may use (affinity set capped by the cgroup quota), divided across the contexts streaming at
+    once, instead of hardware_concurrency() per context. On the driver's boxes (16 CPUs granted of
+    256) 8 contexts get 2 copy threads a site each, not 16 each."""
+    L = bmh.lib()
+    assert L.bmh_host_cpus() == _cgroup_cpus()
+    assert L.bmh_copy_threads(8, 16) == 2
+    assert L.bmh_copy_threads(1, 16) == 16
+    assert L.bmh_copy_threads(8, 256) == 16
+    assert L.bmh_copy_threads(16, 8) == 1
+    assert L.bmh_copy_threads(3, 16) == 5
+    assert L.bmh_copy_threads(0, 16) == 16  # no share given: one context
+    assert L.bmh_copy_threads(1, 0) == min(16, _cgroup_cpus())
+    # 8 contexts under a 16-CPU quota: at most 2 sites x 8 contexts x 2 threads = 32 copy threads
+    assert 2 * 8 * L.bmh_copy_threads(8, 16) <= 2 * 16
