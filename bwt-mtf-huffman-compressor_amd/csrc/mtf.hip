@@ -367,11 +367,14 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
         }
         uint32_t t = plo[j] | (__builtin_amdgcn_ubfe(pe[j], c & 31u, 1u) << 8);
         if (j >= 1) t = c == sym(j - 1) ? pslot : t;
-        const uint32_t am = kOffMarks + ((t >> 6) << 9) + l8;
-        const uint64_t W = lds_u64(s, am);
+        // marks word w = t >> 6 at byte (w << 9) | 8l, its 32-bit half (t >> 5) & 1 at + 4, the
+        // word counts' byte at bit 8w
+        const uint32_t t3 = t >> 3;
+        const uint32_t am = ((t << 3) & 0xE00u) | l8;
+        const uint64_t W = lds_u64(s, kOffMarks + am);
         const uint32_t rw = rank_words(C, t);
-        atomicXor((uint32_t *)(s + am + ((t >> 3) & 4u)), 1u << (t & 31u));
-        C += ~0ull << ((t >> 3) & 0x38u);
+        atomicXor((uint32_t *)(s + kOffMarks + (am | (t3 & 4u))), 1u << (t & 31u));
+        C += ~0ull << (t3 & 0x38u);
         atomicOr((uint32_t *)(s + amn + 4 * (j >> 5)), 1u << (j & 31));
         C += cinc;
         s[a8_of(c, l4)] = (uint8_t)slot;
@@ -406,14 +409,17 @@ __device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t l
 }
 
 // The window is full (slot 512 reached): every symbol's new slot is the number of marks below its
-// slot (0..255, order kept): the marks in the words below (byte prefix sums of C; a byte only
-// overflows past the last marked word, which no symbol reads) + the marks below it in its word.
+// slot (0..255, order kept): the marks in the words below (byte w of P, the prefix sums of C's
+// bytes, picked by a v_perm byte select; a byte only overflows past the last marked word, which no
+// symbol reads) + the marks at or below it in its word (one left shift moves them to the top)
+// minus its own. About 12 VALU and one 8-byte LDS read a symbol, every 256 symbols.
 __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_t l8, uint64_t &C)
 {
     uint64_t P = C << 8;
     P += P << 8;
     P += P << 16;
     P += P << 32;
+    const uint32_t Plo = (uint32_t)P, Phi = (uint32_t)(P >> 32);
 #ifndef BMH_PROBE_NORENUM  // timing probe: renumbering skipped (wrong output)
 #pragma nounroll
     for (uint32_t w = 0; w < 8; ++w) {  // symbols 32w .. 32w + 31
@@ -427,12 +433,15 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
 #pragma unroll
             for (uint32_t b = 0; b < 4; ++b) {
                 const uint32_t k = 4 * j + b;
-                const uint32_t t = ((tw[j] >> (8 * b)) & 255u) | (((e >> k) & 1u) << 8);
-                const uint64_t W = lds_u64(s, kOffMarks + ((t >> 6) << 9) + l8);
-                const uint64_t below = W & ((1ull << (t & 63u)) - 1u);
-                const uint32_t nb = (uint32_t)(P >> ((t >> 3) & 0x38u)) & 255u;
-                nwd |= ((uint32_t)__builtin_popcount((uint32_t)(below >> 32)) + (uint32_t)__builtin_popcount((uint32_t)below) + nb)
-                       << (8 * b);
+                const uint32_t ebit = (k <= 8 ? e << (8 - k) : e >> (k - 8)) & 0x100u;
+                const uint32_t t = ((tw[j] >> (8 * b)) & 255u) | ebit;
+                const uint32_t wd = t >> 6;
+                const uint64_t W = lds_u64(s, kOffMarks + (wd << 9) + l8);
+                const uint64_t upto = W << ((t ^ 63u) & 63u);  // marks at or below t, at the top
+                const uint32_t pw = __builtin_amdgcn_perm(Phi, Plo, wd | 0x0C0C0C00u);
+                const uint32_t nb = (uint32_t)__builtin_popcount((uint32_t)(upto >> 32)) +
+                                    (uint32_t)__builtin_popcount((uint32_t)upto) + pw - 1u;
+                nwd |= (nb & 255u) << (8 * b);
             }
             *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = nwd;
         }
