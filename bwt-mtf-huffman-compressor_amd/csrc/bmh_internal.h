@@ -117,8 +117,6 @@ struct Ctx {
     // sync (bwt_spec_ok) and encodes the batch again the waiting way if any list work was left
     uint32_t *probe_host = nullptr, probe_cap = 0;  // dense_batch's census (pinned, written by the kernel)
     hipEvent_t probe_ev = nullptr;
-    uint32_t *run_cnt_host = nullptr;  // run path: doubling rounds' group counts (pinned), read one round late
-    hipEvent_t run_ev[2] = {};
     void *dbl_cnt_host = nullptr;  // rank doubling: two rounds' counters (pinned), read one round late
     hipEvent_t dbl_ev[2] = {};
     uint64_t pre_sig = 0;  // bwt_batch_core's prologue already launched for this input + layout

@@ -158,7 +158,7 @@ __device__ __forceinline__ uint32_t head_bits16(const uint8_t *__restrict__ t, u
     return f;
 }
 // One workgroup: exclusive prefix (op = sum, or max with identity 0) of cnt[0..m) into out.
-// gate (doubling rounds, k_round_gate): non-null and set -> the round is past its last, no work
+// gate: non-null and set -> no work (unused since round 6's active-run doubling; kept for the sorts)
 #define RUN_GATED(gate) \
     if ((gate) && *(gate)) return
 template <bool MAX>
@@ -423,29 +423,201 @@ __global__ __launch_bounds__(256) void k_brun_keys(const uint8_t *__restrict__ i
     idx[i] = i;
 }
 
-// Start of a doubling round: cnt[0] = the previous round's group count. All groups distinct ->
-// cnt[1] (the gate) set and the round's kernels return at once; else the count restarts.
-__global__ void k_round_gate(uint32_t *cnt, uint32_t M)
+// ---- prefix doubling over the still-tied runs only (round 6). After a round,
+// a run whose rank group is a singleton is finished (its rank is its final slot); the next round
+// sorts only the members of groups of two or more (the "active" runs, listed in `act`) by
+// (rank_i, rank_{i+h}). The members of one old group stay contiguous in the sorted list, so a
+// member's new rank = its old group's first slot + (its new group's first index - its old group's
+// first index) in the list, the first-slot ranks a full re-sort would give. pic (76 K runs) keeps
+// 76 K, 72 K, 28 K, 6 K, 1.4 K, 342 and 72 runs active in its seven rounds: the rounds over more
+// than kTailMax runs are multi-launch (keys, radix sort, rank + compaction: one host wait each),
+// and every round after that runs inside ONE single-workgroup launch (k_act_tail).
+
+// key = rank_i << bits | rank_{i + h} (cyclic in the run's block), value i, for the active runs
+// (act null: runs 0 .. m - 1)
+__global__ __launch_bounds__(256) void k_act_keys(const RBlk *__restrict__ tab, const uint32_t *__restrict__ rblk,
+                                                  const uint32_t *__restrict__ rank, const uint32_t *__restrict__ act,
+                                                  uint32_t m, uint32_t h, uint32_t bits, uint64_t *__restrict__ key,
+                                                  uint32_t *__restrict__ idx)
 {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    if (e >= m) return;
+    const uint32_t i = act ? act[e] : e;
+    const RBlk B = tab[rblk[i]];
+    const uint32_t j = B.R + (uint32_t)(((uint64_t)(i - B.R) + h) % B.m);
+    key[e] = (uint64_t)rank[i] << bits | rank[j];
+    idx[e] = i;
+}
+
+// Slots [j0, j1) of sorted keys sk[0, m): the last new-group head and the last old-group start
+// (0 when none: slot 0 is both) and the survivors (slots whose new group has two or more members).
+__device__ __forceinline__ void act_slots(const uint64_t *sk, uint32_t m, uint32_t bits, uint32_t j0, uint32_t j1,
+                                          uint32_t &lh, uint32_t &lg, uint32_t &sv)
+{
+    lh = lg = sv = 0;
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint64_t k = sk[j];
+        const bool nh = j == 0 || k != sk[j - 1];
+        const bool ng = j == 0 || (k >> bits) != (sk[j - 1] >> bits);
+        const bool nn = j + 1 == m || sk[j + 1] != k;
+        lh = nh ? j : lh;
+        lg = ng ? j : lg;
+        sv += !(nh && nn);
+    }
+}
+// per tile of kPrimTile sorted slots: its last head, last old-group start and survivor count
+__global__ __launch_bounds__(256) void k_act_tiles(const uint64_t *__restrict__ sk, uint32_t m, uint32_t bits,
+                                                   uint32_t *__restrict__ tH, uint32_t *__restrict__ tG,
+                                                   uint32_t *__restrict__ tC)
+{
+    __shared__ uint32_t s_h[4], s_g[4], s_c[4];
+    const uint32_t j0 = min(m, blockIdx.x * kPrimTile + 16u * threadIdx.x);
+    uint32_t lh, lg, sv;
+    act_slots(sk, m, bits, j0, min(m, j0 + 16u), lh, lg, sv);
+    lh = wave_incl_max(lh);
+    lg = wave_incl_max(lg);
+    sv = wave_sum_dpp(sv);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 63u) {
+        s_h[w] = lh;
+        s_g[w] = lg;
+        s_c[w] = sv;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t stop = cnt[0] >= M;
-        cnt[1] = stop;
-        if (!stop) cnt[0] = 0;
+        tH[blockIdx.x] = max(max(s_h[0], s_h[1]), max(s_h[2], s_h[3]));
+        tG[blockIdx.x] = max(max(s_g[0], s_g[1]), max(s_g[2], s_g[3]));
+        tC[blockIdx.x] = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    }
+}
+// one workgroup: the tiles' exclusive max prefixes (tH, tG) and exclusive sum (tC), in place;
+// cnt[0] = survivors of the round
+__global__ __launch_bounds__(1024) void k_act_scan(uint32_t *__restrict__ tH, uint32_t *__restrict__ tG,
+                                                   uint32_t *__restrict__ tC, uint32_t nt, uint32_t *__restrict__ cnt)
+{
+    __shared__ uint32_t s_tmp[17];
+    const uint32_t per = (nt + 1023) / 1024, t = threadIdx.x, a = min(nt, t * per), e = min(nt, a + per);
+    uint32_t mh = 0, mg = 0, sc = 0;
+    for (uint32_t i = a; i < e; ++i) {
+        mh = max(mh, tH[i]);
+        mg = max(mg, tG[i]);
+        sc += tC[i];
+    }
+    uint32_t rh = block_excl_max<1024>(mh, s_tmp);
+    uint32_t rg = block_excl_max<1024>(mg, s_tmp);
+    uint32_t tot;
+    uint32_t rc = block_excl_sum<1024>(sc, s_tmp, &tot);
+    for (uint32_t i = a; i < e; ++i) {
+        const uint32_t h = tH[i], g = tG[i], c = tC[i];
+        tH[i] = rh;
+        tG[i] = rg;
+        tC[i] = rc;
+        rh = max(rh, h);
+        rg = max(rg, g);
+        rc += c;
+    }
+    if (t == 0) cnt[0] = tot;
+}
+// new ranks of the sorted active runs (rank[sv[j]]) and the survivors, in sorted order, to act_out
+__global__ __launch_bounds__(256) void k_act_rank(const uint64_t *__restrict__ sk, const uint32_t *__restrict__ sv,
+                                                  uint32_t m, uint32_t bits, const uint32_t *__restrict__ oH,
+                                                  const uint32_t *__restrict__ oG, const uint32_t *__restrict__ oC,
+                                                  uint32_t *__restrict__ rank, uint32_t *__restrict__ act_out)
+{
+    __shared__ uint32_t s_tmp[8];
+    const uint32_t j0 = min(m, blockIdx.x * kPrimTile + 16u * threadIdx.x), j1 = min(m, j0 + 16u);
+    uint32_t lh, lg, nsv;
+    act_slots(sk, m, bits, j0, j1, lh, lg, nsv);
+    uint32_t gh = max(oH[blockIdx.x], block_excl_max<256>(lh, s_tmp));
+    uint32_t gg = max(oG[blockIdx.x], block_excl_max<256>(lg, s_tmp));
+    uint32_t pos = oC[blockIdx.x] + block_excl_sum1<256>(nsv, s_tmp);
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint64_t k = sk[j];
+        const bool nh = j == 0 || k != sk[j - 1];
+        const bool ng = j == 0 || (k >> bits) != (sk[j - 1] >> bits);
+        const bool nn = j + 1 == m || sk[j + 1] != k;
+        gh = nh ? j : gh;
+        gg = ng ? j : gg;
+        const uint32_t i = sv[j];
+        rank[i] = (uint32_t)(k >> bits) + gh - gg;
+        if (!(nh && nn)) act_out[pos++] = i;
     }
 }
 
-// (rank_i, rank of the run h further on in the same block, cyclic) packed in 2 * bits, value i
-__global__ __launch_bounds__(256) void k_bpair_keys(const RBlk *__restrict__ tab, const uint32_t *__restrict__ rblk,
-                                                    const uint32_t *__restrict__ rank, uint32_t M, uint32_t h, uint32_t bits,
-                                                    uint64_t *__restrict__ key, uint32_t *__restrict__ idx, const uint32_t *gate)
+// Every remaining round in one launch, once at most kTailMax runs are active: one workgroup keeps
+// the active list in LDS; a round builds the keys (ranks read at agent scope, past this CU's L1:
+// the previous round's rank stores are this workgroup's own), sorts them with a bitonic network in
+// LDS (equal keys are one group, so the order among them does not matter), writes the new ranks
+// and compacts the survivors, until none is left or h reaches the longest run sequence.
+constexpr uint32_t kTailMax = 8192, kTailNT = 1024;
+__global__ __launch_bounds__(kTailNT) void k_act_tail(const RBlk *__restrict__ tab, const uint32_t *__restrict__ rblk,
+                                                      uint32_t *rank, const uint32_t *__restrict__ act, uint32_t m,
+                                                      uint32_t h, uint32_t maxm, uint32_t bits)
 {
-    RUN_GATED(gate);
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= M) return;
-    const RBlk B = tab[rblk[i]];
-    const uint32_t j = B.R + (uint32_t)(((uint64_t)(i - B.R) + h) % B.m);
-    key[i] = (uint64_t)rank[i] << bits | rank[j];
-    idx[i] = i;
+    __shared__ uint64_t s_key[kTailMax];
+    __shared__ uint32_t s_val[kTailMax], s_act[kTailMax];
+    __shared__ uint32_t s_tmp[kTailNT / 64 + 1];
+    const uint32_t t = threadIdx.x;
+    for (uint32_t e = t; e < m; e += kTailNT) s_act[e] = act ? act[e] : e;
+    __syncthreads();
+    while (m > 0 && h < maxm) {  // m, h: workgroup-uniform
+        uint32_t n2 = 1;
+        while (n2 < m) n2 <<= 1;
+        for (uint32_t e = t; e < n2; e += kTailNT) {
+            uint64_t k = ~0ull;
+            uint32_t i = 0;
+            if (e < m) {
+                i = s_act[e];
+                const RBlk B = tab[rblk[i]];
+                const uint32_t j = B.R + (uint32_t)(((uint64_t)(i - B.R) + h) % B.m);
+                const uint32_t ri = __hip_atomic_load(rank + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t rj = __hip_atomic_load(rank + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                k = (uint64_t)ri << bits | rj;
+            }
+            s_key[e] = k;
+            s_val[e] = i;
+        }
+        __syncthreads();
+        for (uint32_t kk = 2; kk <= n2; kk <<= 1)
+            for (uint32_t jj = kk >> 1; jj > 0; jj >>= 1) {
+                for (uint32_t i = t; i < n2; i += kTailNT) {
+                    const uint32_t ixj = i ^ jj;
+                    if (ixj > i) {
+                        const uint64_t a = s_key[i], b = s_key[ixj];
+                        if ((a > b) == ((i & kk) == 0)) {
+                            s_key[i] = b;
+                            s_key[ixj] = a;
+                            const uint32_t v = s_val[i];
+                            s_val[i] = s_val[ixj];
+                            s_val[ixj] = v;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        const uint32_t per = (m + kTailNT - 1) / kTailNT, j0 = min(m, t * per), j1 = min(m, j0 + per);
+        uint32_t lh, lg, nsv;
+        act_slots(s_key, m, bits, j0, j1, lh, lg, nsv);
+        uint32_t gh = block_excl_max<kTailNT>(lh, s_tmp);
+        uint32_t gg = block_excl_max<kTailNT>(lg, s_tmp);
+        uint32_t tot;
+        uint32_t pos = block_excl_sum<kTailNT>(nsv, s_tmp, &tot);
+        for (uint32_t j = j0; j < j1; ++j) {
+            const uint64_t k = s_key[j];
+            const bool nh = j == 0 || k != s_key[j - 1];
+            const bool ng = j == 0 || (k >> bits) != (s_key[j - 1] >> bits);
+            const bool nn = j + 1 == m || s_key[j + 1] != k;
+            gh = nh ? j : gh;
+            gg = ng ? j : gg;
+            const uint32_t i = s_val[j];
+            rank[i] = (uint32_t)(k >> bits) + gh - gg;
+            if (!(nh && nn)) s_act[pos++] = i;
+        }
+        __threadfence();  // the new ranks reach the L2 before the next round's agent-scope reads
+        __syncthreads();
+        m = tot;
+        h *= 2;
+    }
 }
 
 // position keys (header comment) below the block index, value p: grid (tiles of 256, blocks)
@@ -504,7 +676,7 @@ inline uint32_t bits_for(uint32_t v)  // bits holding 0 .. v
 }
 
 struct RunWs {
-    uint32_t *H, *rblk, *idx, *idx2, *rank, *cnt, *tcnt, *toff, *rowpre, *dtot;
+    uint32_t *H, *rblk, *idx, *idx2, *rank, *act, *act2, *cnt, *tcnt, *toff, *tC, *rowpre, *dtot;
     uint64_t *key, *key2;
     uint64_t *pkey, *pkey2;
     uint32_t *pval, *pval2;
@@ -517,14 +689,14 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 RunWs run_ws(Ctx *c, uint64_t N, uint32_t M, uint32_t NT, uint32_t B)
 {
     const size_t mm = std::max(M, 1u), nt = std::max<size_t>(NT, cdiv(std::max<uint64_t>(N, 1), kRsTile));
-    const size_t sizes[] = {align256(mm * 4) * 5 + 256, align256(nt * 4) * 2, align256(kRsBins * nt * 4) + kRsBins * 4,
+    const size_t sizes[] = {align256(mm * 4) * 7 + 256, align256(nt * 4) * 3, align256(kRsBins * nt * 4) + kRsBins * 4,
                             align256(mm * 8) * 2, align256((size_t)N * 8) * 2, align256((size_t)N * 4) * 2,
                             align256((size_t)B * sizeof(RBlk))};
     size_t total = 0;
     for (size_t z : sizes) total += z;
     uint8_t *p = (uint8_t *)c->get(WS_RUNS, total);
     RunWs w;
-    uint32_t **u32s[] = {&w.H, &w.rblk, &w.idx, &w.idx2, &w.rank};
+    uint32_t **u32s[] = {&w.H, &w.rblk, &w.idx, &w.idx2, &w.rank, &w.act, &w.act2};
     for (auto q : u32s) {
         *q = (uint32_t *)p;
         p += align256(mm * 4);
@@ -534,6 +706,8 @@ RunWs run_ws(Ctx *c, uint64_t N, uint32_t M, uint32_t NT, uint32_t B)
     w.tcnt = (uint32_t *)p;
     p += align256(nt * 4);
     w.toff = (uint32_t *)p;
+    p += align256(nt * 4);
+    w.tC = (uint32_t *)p;
     p += align256(nt * 4);
     w.rowpre = (uint32_t *)p;
     p += align256(kRsBins * nt * 4);
@@ -556,7 +730,7 @@ RunWs run_ws(Ctx *c, uint64_t N, uint32_t M, uint32_t NT, uint32_t B)
 }
 
 // Ranks of sorted keys sk (m of them, values sidx): rank[sidx[j]] = first slot of sk[j]'s
-// group; the group count lands in w.cnt[0] (zeroed before: by a memset, or by k_round_gate).
+// group; the group count lands in w.cnt[0] (zeroed before by a memset).
 void rank_groups_async(Ctx *c, RunWs &w, const uint64_t *sk, const uint32_t *sidx, uint32_t m, const uint32_t *gate)
 {
     const uint32_t nt = cdiv(m, kPrimTile);
@@ -639,38 +813,35 @@ void run_blocks_batch(Ctx *c, const uint8_t *in, const std::vector<uint64_t> &of
         sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 33 + bb);
         const uint32_t groups = rank_groups(c, w, w.key2, w.idx2, M, h_cnt);
         const uint32_t bits = bits_for(M - 1);
-        // prefix doubling over the run sequence: round h sorts (rank_i, rank_{i+h}) and re-ranks,
-        // until all ranks differ (or h >= the longest run sequence). The host reads each round's
-        // group count one round late: round h + 1 is queued before the wait for round h's count,
-        // gated on the device by that count (k_round_gate), so the GPU never idles on the wait;
-        // the one round queued past the last costs its empty launches.
+        // prefix doubling over the run sequence: round h sorts (rank_i, rank_{i+h}) of the runs
+        // still tied and re-ranks them, until none is tied (or h >= the longest run sequence);
+        // rounds over more than kTailMax runs take one host wait each, the rest one launch
         if (groups < M && maxm > 1) {
-            if (!c->run_cnt_host) BMH_HIP(hipHostMalloc((void **)&c->run_cnt_host, 64, hipHostMallocDefault));
-            for (auto &e : c->run_ev)
-                if (!e) BMH_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            const uint32_t *gate = w.cnt + 1;
-            auto launch_round = [&](uint64_t h, int slot) {
-                BMH_LAUNCH(c, "bwt_run_groups", k_round_gate, 1, 64, 0, w.cnt, M);
-                BMH_LAUNCH(c, "bwt_run_keys", k_bpair_keys, cdiv(M, 256), 256, 0, w.tab, w.rblk, w.rank, M, (uint32_t)h,
-                           bits, w.key, w.idx, gate);
-                const bool in_key = sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, M, 2 * bits, gate, true);
-                rank_groups_async(c, w, in_key ? w.key : w.key2, in_key ? w.idx : w.idx2, M, gate);
-                BMH_HIP(hipMemcpyAsync(c->run_cnt_host + slot, w.cnt, 4, hipMemcpyDeviceToHost, c->stream));
-                BMH_HIP(hipEventRecord(c->run_ev[slot], c->stream));
-            };
             uint64_t h = 1;
-            launch_round(h, 0);
-            for (int r = 0;; ++r) {
-                const bool more = 2 * h < maxm;
-                if (more) launch_round(2 * h, (r + 1) & 1);
-                for (;;) {  // spin: a blocking wait can sleep the host thread for milliseconds
-                    const hipError_t e = hipEventQuery(c->run_ev[r & 1]);
-                    if (e == hipSuccess) break;
-                    if (e != hipErrorNotReady) BMH_HIP(e);
-                }
-                if (c->run_cnt_host[r & 1] >= M || !more) break;  // a queued round past this is gated
+            uint32_t ma = M;
+            const uint32_t *act = nullptr;  // all runs
+            uint32_t *abuf[2] = {w.act, w.act2};
+            for (int ab = 0; ma > kTailMax; ab ^= 1) {
+                BMH_LAUNCH(c, "bwt_run_keys", k_act_keys, cdiv(ma, 256), 256, 0, w.tab, w.rblk, w.rank, act, ma,
+                           (uint32_t)h, bits, w.key, w.idx);
+                const bool in_key = sort_pairs(c, w, w.key, w.key2, w.idx, w.idx2, ma, 2 * bits, nullptr, true);
+                const uint64_t *sk = in_key ? w.key : w.key2;
+                const uint32_t *sv = in_key ? w.idx : w.idx2;
+                const uint32_t nt = cdiv(ma, kPrimTile);
+                BMH_LAUNCH(c, "bwt_run_groups", k_act_tiles, nt, 256, 0, sk, ma, bits, w.tcnt, w.toff, w.tC);
+                BMH_LAUNCH(c, "bwt_run_scan", k_act_scan, 1, 1024, 0, w.tcnt, w.toff, w.tC, nt, w.cnt);
+                BMH_LAUNCH(c, "bwt_run_groups", k_act_rank, nt, 256, 0, sk, sv, ma, bits, w.tcnt, w.toff, w.tC, w.rank,
+                           abuf[ab]);
+                c->d2h(h_cnt, w.cnt, 4);
+                c->sync();
+                ma = *h_cnt;
+                act = abuf[ab];
                 h *= 2;
+                if (h >= maxm) ma = 0;  // the runs still tied are identical rotations
             }
+            if (ma > 0)
+                BMH_LAUNCH(c, "bwt_run_tail", k_act_tail, 1, kTailNT, 0, w.tab, w.rblk, w.rank, act, ma, (uint32_t)h,
+                           maxm, bits);
         }
         const dim3 pgrid(cdiv(maxn, 256), B);
         BMH_LAUNCH(c, "bwt_run_place", k_bpos_keys, pgrid, 256, 0, in, w.tab, w.H, w.rank, w.pkey, w.pval);

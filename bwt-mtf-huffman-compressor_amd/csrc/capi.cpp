@@ -924,9 +924,6 @@ void bmh_ctx_destroy(bmh_ctx *c)
     if (c->arena) (void)hipHostFree(c->arena);
     if (c->probe_host) (void)hipHostFree(c->probe_host);
     if (c->probe_ev) (void)hipEventDestroy(c->probe_ev);
-    if (c->run_cnt_host) (void)hipHostFree(c->run_cnt_host);
-    for (auto e : c->run_ev)
-        if (e) (void)hipEventDestroy(e);
     if (c->dbl_cnt_host) (void)hipHostFree(c->dbl_cnt_host);
     for (auto e : c->dbl_ev)
         if (e) (void)hipEventDestroy(e);

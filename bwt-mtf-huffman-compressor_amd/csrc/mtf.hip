@@ -306,10 +306,24 @@ __device__ __forceinline__ uint32_t rank_words(uint64_t C, uint32_t t)
     const uint32_t r = __builtin_amdgcn_sad_u8((uint32_t)C & (uint32_t)M, 0u, 0xFFFFFFFFu);
     return __builtin_amdgcn_sad_u8((uint32_t)(C >> 32) & (uint32_t)(M >> 32), 0u, r);
 }
+// v_bcnt_u32_b32 with its accumulator (the compiler emits bcnt(x, 0) twice and an add3)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc)
+{
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 __device__ __forceinline__ uint32_t rank_bits(uint64_t W, uint32_t t, uint32_t acc)
 {
     const uint64_t ws = W >> (t & 63u);
-    return (uint32_t)__builtin_popcount((uint32_t)(ws >> 32)) + (uint32_t)__builtin_popcount((uint32_t)ws) + acc;
+    return bcnt_acc((uint32_t)(ws >> 32), bcnt_acc((uint32_t)ws, acc));
+}
+// (a & 4) | b in one v_and_or_b32 (the compiler splits it into an and and an add)
+__device__ __forceinline__ uint32_t and4_or(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, 4, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
 // MTF of symbol c at the wave-uniform slot `slot` (256..511). Returns the index; the state update
@@ -373,7 +387,7 @@ __device__ __forceinline__ void mtf_whole(const uint4 (&in)[4], uint32_t now, ui
         const uint32_t am = ((t << 3) & 0xE00u) | l8;
         const uint64_t W = lds_u64(s, kOffMarks + am);
         const uint32_t rw = rank_words(C, t);
-        atomicXor((uint32_t *)(s + kOffMarks + (am | (t3 & 4u))), 1u << (t & 31u));
+        atomicXor((uint32_t *)(s + kOffMarks + and4_or(t3, am)), 1u << (t & 31u));
         C += ~0ull << (t3 & 0x38u);
         atomicOr((uint32_t *)(s + amn + 4 * (j >> 5)), 1u << (j & 31));
         C += cinc;
@@ -409,17 +423,21 @@ __device__ __forceinline__ void window_reset(uint8_t *s, uint32_t l4, uint32_t l
 }
 
 // The window is full (slot 512 reached): every symbol's new slot is the number of marks below its
-// slot (0..255, order kept): the marks in the words below (byte w of P, the prefix sums of C's
-// bytes, picked by a v_perm byte select; a byte only overflows past the last marked word, which no
-// symbol reads) + the marks at or below it in its word (one left shift moves them to the top)
-// minus its own. About 12 VALU and one 8-byte LDS read a symbol, every 256 symbols.
+// slot t (0..255, order kept) = the marks in words 0..w (w = t >> 6) minus the marks of word w at
+// or above t's bit: Q[w] - popcount(W_w >> (t & 63)), with Q the byte prefix sums of C shifted one
+// word down (Q[7] = 256 = 0 mod 256; a byte only overflows past the last marked word, which no
+// symbol reads), picked by a v_perm byte select. The four symbols of a stamp dword get their word
+// indices in one SIMD-within-a-register step (their epoch bits spread by one multiply), and their
+// new bytes are packed by three v_perm. About 10 VALU and one 8-byte LDS read a symbol, every 256
+// symbols (round 5's form: 16 VALU).
 __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_t l8, uint64_t &C)
 {
     uint64_t P = C << 8;
     P += P << 8;
     P += P << 16;
     P += P << 32;
-    const uint32_t Plo = (uint32_t)P, Phi = (uint32_t)(P >> 32);
+    const uint64_t Q = P >> 8;  // byte w = marks in words 0..w
+    const uint32_t Qlo = (uint32_t)Q, Qhi = (uint32_t)(Q >> 32);
 #ifndef BMH_PROBE_NORENUM  // timing probe: renumbering skipped (wrong output)
 #pragma nounroll
     for (uint32_t w = 0; w < 8; ++w) {  // symbols 32w .. 32w + 31
@@ -429,21 +447,22 @@ __device__ __forceinline__ void window_renumber(uint8_t *s, uint32_t l4, uint32_
         for (uint32_t j = 0; j < 8; ++j) tw[j] = lds_u32(s, ((8 * w + j) << 8) + l4);
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
-            uint32_t nwd = 0;
+            // byte b of wd4 = word index of symbol 4j + b: stamp bits 6..7, epoch bit as bit 2
+            const uint32_t spread = (((e >> (4 * j)) & 15u) * 0x00810204u) & 0x04040404u;
+            const uint32_t wd4 = ((tw[j] >> 6) & 0x03030303u) | spread;
+            uint32_t nb[4];
 #pragma unroll
             for (uint32_t b = 0; b < 4; ++b) {
-                const uint32_t k = 4 * j + b;
-                const uint32_t ebit = (k <= 8 ? e << (8 - k) : e >> (k - 8)) & 0x100u;
-                const uint32_t t = ((tw[j] >> (8 * b)) & 255u) | ebit;
-                const uint32_t wd = t >> 6;
-                const uint64_t W = lds_u64(s, kOffMarks + (wd << 9) + l8);
-                const uint64_t upto = W << ((t ^ 63u) & 63u);  // marks at or below t, at the top
-                const uint32_t pw = __builtin_amdgcn_perm(Phi, Plo, wd | 0x0C0C0C00u);
-                const uint32_t nb = (uint32_t)__builtin_popcount((uint32_t)(upto >> 32)) +
-                                    (uint32_t)__builtin_popcount((uint32_t)upto) + pw - 1u;
-                nwd |= (nb & 255u) << (8 * b);
+                const uint32_t sel = wd4 >> (8 * b);  // byte 0 = w (higher bytes: unused result bytes)
+                const uint32_t sh = tw[j] >> (8 * b);  // low 6 bits = t & 63
+                const uint64_t W = lds_u64(s, kOffMarks + (((sel & 7u) << 9) | l8));
+                const uint64_t at = W >> (sh & 63u);
+                nb[b] = __builtin_amdgcn_perm(Qhi, Qlo, sel) - (uint32_t)__builtin_popcount((uint32_t)(at >> 32)) -
+                        (uint32_t)__builtin_popcount((uint32_t)at);
             }
-            *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = nwd;
+            const uint32_t p01 = __builtin_amdgcn_perm(nb[1], nb[0], 0x0C0C0400u);
+            const uint32_t p23 = __builtin_amdgcn_perm(nb[3], nb[2], 0x0C0C0400u);
+            *(uint32_t *)(s + ((8 * w + j) << 8) + l4) = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
         }
     }
 #endif
