@@ -259,7 +259,8 @@ class Context:
         return int(lib().bmh_ctx_spec_fallbacks(self.h))
 
     # ---- tuning options (include/bmh.h BMH_OPT_*; 0 restores the library's rule)
-    OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5, "one_pipeline": 6}
+    OPTIONS = {"pipelines": 1, "stream_batch": 2, "max_batch": 3, "mtf_chunk": 4, "check_lists": 5, "one_pipeline": 6,
+               "copy_threads": 7}
 
     def set_option(self, name: str, value: int) -> None:
         _check(lib().bmh_ctx_set_option(self.h, self.OPTIONS[name], int(value)), f"set_option({name})")

@@ -98,7 +98,7 @@ struct Ctx {
     // tuning options (bmh_ctx_set_option; 0 = the library's rule); sub-pipelines and the side
     // context copy their parent's at every call
     struct Options {
-        uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0, one_pipeline = 0;
+        uint64_t pipelines = 0, stream_batch = 0, max_batch = 0, mtf_chunk = 0, check_lists = 0, one_pipeline = 0, copy_threads = 0;
     } opt;
     uint32_t last_pipelines = 0;  // pipelines of the last device batch encode (encode_blocks)
     uint64_t zipf_resume_tok0 = 0, zipf_resume_base = 0;  // synth_zipf: start of its last round

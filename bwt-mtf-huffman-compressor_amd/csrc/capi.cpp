@@ -524,7 +524,11 @@ static unsigned copy_threads_for(unsigned cpus, unsigned share)
 {
     return std::max(1u, std::min(16u, cpus / std::max(1u, share)));
 }
-static unsigned copy_threads(const Ctx *c = nullptr) { return copy_threads_for(host_cpus(), c ? c->copy_share : 1u); }
+static unsigned copy_threads(const Ctx *c = nullptr)
+{
+    if (c && c->opt.copy_threads) return (unsigned)c->opt.copy_threads;  // BMH_OPT_COPY_THREADS
+    return copy_threads_for(host_cpus(), c ? c->copy_share : 1u);
+}
 
 // Page-locked (hipHostMalloc'd or hipHostRegister'ed) host range that device `dev`'s DMA engines
 // may read and write directly, so the streaming encoder skips its staging copies. The range is
@@ -1357,6 +1361,10 @@ bmh_status bmh_ctx_set_option(bmh_ctx *c, uint32_t option, uint64_t value)
         break;
     case BMH_OPT_CHECK_LISTS: c->opt.check_lists = value != 0; break;
     case BMH_OPT_ONE_PIPELINE: c->opt.one_pipeline = value != 0; break;
+    case BMH_OPT_COPY_THREADS:
+        if (value > 64) fail(BMH_ERANGE, "set_option: at most 64 copy threads");
+        c->opt.copy_threads = value;
+        break;
     default: fail(BMH_EINVAL, "set_option: unknown option " + std::to_string(option));
     }
     API_END

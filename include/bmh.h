@@ -192,9 +192,11 @@ enum {
     BMH_OPT_MAX_BATCH = 3,    /* largest device batch bytes of the host-buffer paths (default 1 GiB) */
     BMH_OPT_MTF_CHUNK = 4,    /* MTF chunk symbols, 64..4096 (default: adaptive) */
     BMH_OPT_CHECK_LISTS = 5,  /* 1: check every BWT list round and print its census (diagnostic, slow) */
-    BMH_OPT_ONE_PIPELINE = 6  /* 1: run each device batch on one pipeline AFTER the library's own
+    BMH_OPT_ONE_PIPELINE = 6, /* 1: run each device batch on one pipeline AFTER the library's own
                                * decisions (the dense-batch census and its speculative list round
                                * still apply), so a one-stream timing pass runs the default path */
+    BMH_OPT_COPY_THREADS = 7  /* host-buffer paths: copy threads per copy site, 1..64 (default:
+                               * bmh_copy_threads(contexts streaming at once, 0)) */
 };
 bmh_status bmh_ctx_set_option(bmh_ctx *ctx, uint32_t option, uint64_t value);
 

@@ -913,7 +913,7 @@ def test_tuning_options_never_change_records(ctx, oracle):
             ctx.set_option(name, 0)
         data = b"".join(blocks[:12])
         ref = ctx.compress_bytes(data, block_size=1 << 20)
-        for name, v in (("stream_batch", 3 << 20), ("max_batch", 2 << 20)):
+        for name, v in (("stream_batch", 3 << 20), ("max_batch", 2 << 20), ("copy_threads", 2)):
             ctx.set_option(name, v)
             assert ctx.compress_bytes(data, block_size=1 << 20) == ref, name
             assert ctx.decompress_bytes(ref) == data, name
@@ -921,7 +921,7 @@ def test_tuning_options_never_change_records(ctx, oracle):
     finally:
         for name in bmh.Context.OPTIONS:
             ctx.set_option(name, 0)
-    for opt, v, st in ((99, 1, 1), (1, 17, 4), (4, 5000, 4), (4, 10, 4)):
+    for opt, v, st in ((99, 1, 1), (1, 17, 4), (4, 5000, 4), (4, 10, 4), (7, 65, 4)):
         assert bmh.lib().bmh_ctx_set_option(ctx.h, opt, v) == st, (opt, v)
 
 

@@ -6,7 +6,11 @@ the contexts share device 0). The text is the true App. D stream, generated in H
 bmh_synth_zipf_dev and copied to pageable host memory; every record is checked against the
 reference's 512-block manifest (zipf_16m, tests/golden/make_golden.py) and the whole container
 is round-tripped by the GPU decoder (bmh_decompress_dev).
-usage: python tools/config5_run.py [--gib 8] [--contexts 1] [--opts name=value,...]"""
+Per-rank rehearsal of config 5 at N = 8: --gib 1 is one rank's share (64 x 16
+MiB blocks); --pinned puts input and output in page-locked memory (DMA-only copies); --steps
+times several calls; --opts copy_threads=2 gives the staging copies the 2 threads a site that 8
+contexts sharing a 16-CPU quota get (bmh_copy_threads).
+usage: python tools/config5_run.py [--gib 8] [--contexts 1] [--pinned] [--steps 1] [--opts name=value,...]"""
 import argparse
 import ctypes as C
 import hashlib
@@ -25,6 +29,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--gib", type=int, default=8)
 ap.add_argument("--contexts", type=int, default=1)
 ap.add_argument("--opts", default="", help="bmh_ctx_set_option list name=value,...")
+ap.add_argument("--pinned", action="store_true", help="page-locked input and output buffers")
+ap.add_argument("--steps", type=int, default=1)
 a = ap.parse_args()
 n = a.gib << 30
 bs = 16 << 20
@@ -33,7 +39,12 @@ ctxs = [bmh.Context(0) for _ in range(a.contexts)]
 for c in ctxs:
     c.set_options(a.opts)
 t0 = time.perf_counter()
-data = np.empty(n, dtype=np.uint8)
+hold = []
+if a.pinned:
+    hold.append(ctxs[0].alloc_host(n))
+    data = hold[-1].a
+else:
+    data = np.empty(n, dtype=np.uint8)
 piece = 1 << 30
 d = ctxs[0].alloc(piece)
 for off in range(0, n, piece):
@@ -43,7 +54,11 @@ for off in range(0, n, piece):
 d.free()
 gen_s = time.perf_counter() - t0
 cap = int(L.bmh_compress_bound(n, bs))
-out = np.empty(cap, dtype=np.uint8)
+if a.pinned:
+    hold.append(ctxs[0].alloc_host(cap))
+    out = hold[-1].a
+else:
+    out = np.empty(cap, dtype=np.uint8)
 olen = C.c_uint64()
 
 
@@ -60,9 +75,12 @@ def run():
 
 
 run()  # warm-up
-t1 = time.perf_counter()
-run()
-dt = time.perf_counter() - t1
+each = []
+for _ in range(a.steps):
+    t1 = time.perf_counter()
+    run()
+    each.append(time.perf_counter() - t1)
+dt = sorted(each)[len(each) // 2]  # median
 rec = out[: olen.value]
 recs = bmh.container_records(rec)
 man = json.load(open(os.path.join(REPO, "tests", "golden", "manifests", "zipf_16m.json")))
@@ -79,4 +97,5 @@ print(json.dumps({"config": "5: Zipf text, 16 MiB blocks, host buffers in and ou
                   "blocks": len(recs), "contexts": a.contexts, "ms": round(dt * 1e3, 1),
                   "MBps_pcie_inclusive": round(n / dt / 1e6, 1), "ratio": round(olen.value / n, 6),
                   "records_equal_reference_manifest": f"{ref_eq}/{nchk}", "roundtrip_bit_exact": bool(ok),
-                  "decode_s": round(dec_s, 2), "gen_s": round(gen_s, 1)}))
+                  "decode_s": round(dec_s, 2), "gen_s": round(gen_s, 1), "pinned": a.pinned, "opts": a.opts,
+                  "steps_ms": [round(x * 1e3, 1) for x in each], "host_cpus": int(L.bmh_host_cpus())}))

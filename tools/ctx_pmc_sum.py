@@ -50,6 +50,7 @@ for d in sys.argv[1:]:
             for x in xs:
                 for a, v in x[3].items():
                     cn[a] += v / len(xs)
-            parts.append(f"{k[2:]} {dur:.3f}ms " + " ".join(f"{a.replace('_sum', '')}={v:.3g}" for a, v in sorted(cn.items())))
+            mhz = f" clock={cn['GRBM_GUI_ACTIVE'] / 8 / (dur * 1e-3) / 1e6:.0f}MHz" if "GRBM_GUI_ACTIVE" in cn else ""
+            parts.append(f"{k[2:]} {dur:.3f}ms{mhz} " + " ".join(f"{a.replace('_sum', '')}={v:.3g}" for a, v in sorted(cn.items())))
         if parts:
             print(f" group {ci}: " + " | ".join(parts))
