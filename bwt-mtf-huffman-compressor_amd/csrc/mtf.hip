@@ -13,15 +13,15 @@
 //                tm[s] = slot of the last access of symbol s in a 512-slot window, and a slot
 //                bit is set iff it is some symbol's last access (always 256 marks). The MTF
 //                index of c is the number of marks above tm[c] (symbols used more recently),
-//                counted in two levels: whole superwords above (4 byte counters in a VGPR),
-//                words above inside c's superword (byte counters in LDS), bits above inside
-//                c's word (one popcount). An access clears one mark and sets the next slot —
+//                counted in two levels: the marks of the 64-slot words above (8 byte counters
+//                in a VGPR pair, one masked byte sum), the marks above in c's word (one 64-bit
+//                shift, two popcounts). An access clears one mark and sets the next slot —
 //                O(1) work instead of moving up to 255 list entries; the window is renumbered
 //                every 256 symbols (new slot = marks below the old one). Stamps are stored as a
-//                byte + an "accessed this epoch" bit (368 B of state per lane), one-wave
-//                workgroups, branch-free steps (~34 VALU + 10 LDS ops per symbol; 2.9 ms per
-//                GiB on MI355X, vs 28-40 ms for whole-wave list updates,
-//                tools/microbench/mtf_variants.hip).
+//                byte + an "accessed this epoch" bit (352 B of state per lane: seven one-wave
+//                workgroups a CU), branch-free steps (~30 VALU + 7 LDS ops per symbol, ~10 VALU
+//                a symbol per renumbering; 1.89 ms per GiB on MI355X, round 5: 2.5 ms with 10
+//                LDS ops and 6 workgroups a CU; whole-wave list updates: 28-40 ms).
 //   4. hist    : freq + first occurrence of each MTF value per block (LDS atomics).
 #include "bmh_internal.h"
 
