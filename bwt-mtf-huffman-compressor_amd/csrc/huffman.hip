@@ -88,27 +88,32 @@ __device__ __forceinline__ uint32_t internal_rank(uint32_t L, uint32_t v)
     return L <= 128u ? (v == 2u ? 127u : v - 2u * (uint32_t)(v <= 127u)) : v - 66u * (uint32_t)(v <= 192u);
 }
 
-// Rank of each of this lane's keys (slots lane + 64k) among the 256 keys of s_keys (padding
-// entries ~0): the number of smaller keys. Keys are read two at a time, 8 loads in flight.
-__device__ __forceinline__ void rank4_u64(const uint64_t *s_keys, uint32_t lane, uint32_t (&pos)[4])
+// Rank of key x among the 256 keys of s_keys (padding entries ~0): the number of smaller keys.
+// Every thread of the workgroup reads the same two keys at a time (LDS broadcast), 8 in flight.
+__device__ __forceinline__ uint32_t rank_u64(const uint64_t *s_keys, uint64_t x)
 {
-    uint64_t mine[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        mine[k] = s_keys[lane + 64 * k];
-        pos[k] = 0;
-    }
+    uint32_t pos = 0;
 #pragma unroll 8
     for (uint32_t u = 0; u < 256; u += 2) {
         const uint4 v = *(const uint4 *)&s_keys[u];
         const uint64_t a = ((uint64_t)v.y << 32) | v.x, c = ((uint64_t)v.w << 32) | v.z;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) pos[k] += (uint32_t)(a < mine[k]) + (uint32_t)(c < mine[k]);
+        pos += (uint32_t)(a < x) + (uint32_t)(c < x);
     }
+    return pos;
 }
 
-// grid = nblocks, 64 threads (one wave per block).
-__global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ freq32,
+// The queue phases run on wave 0 alone: LDS traffic between its lanes needs only the wave's own
+// ordering (a fence the compiler cannot move accesses across, then a wave barrier).
+#define WAVE_SYNC()                                          \
+    do {                                                     \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); \
+        __builtin_amdgcn_wave_barrier();                     \
+    } while (0)
+
+// grid = nblocks, 256 threads (four waves per block): the per-symbol and per-leaf phases take a
+// thread each; the queue (a chain of dependent pops) runs on wave 0.
+constexpr uint32_t kHuffThreads = 256;
+__global__ __launch_bounds__(kHuffThreads) void k_huff_build(const uint32_t *__restrict__ freq32,
                                                    const uint32_t *__restrict__ first32,
                                                    const uint32_t *__restrict__ prim, const uint64_t *__restrict__ boffs,
                                                    DevTable *__restrict__ tabs, uint8_t *__restrict__ hdr,
@@ -116,7 +121,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                                                    uint32_t *status, const uint32_t *__restrict__ rbase,
                                                    const uint32_t *__restrict__ ridx, const uint16_t *__restrict__ rrank)
 {
-    __shared__ uint32_t s_freq[256], s_first[256];
+    __shared__ uint32_t s_freq[256];
     __shared__ uint8_t s_order[256];
     __shared__ int16_t s_left[512], s_right[512];
     __shared__ uint64_t s_code[256];
@@ -128,33 +133,25 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __shared__ uint64_t s_lkey[256];                   // leaf keys, then left-aligned leaf codes
     __shared__ uint64_t s_k1[256], s_q2[512];          // leaves in pop order; the pop sequence P
     __shared__ uint32_t s_err;
+    __shared__ uint64_t s_bits;
     uint8_t *s_tree = (uint8_t *)s_tree32;
-    const uint32_t b = blockIdx.x, lane = threadIdx.x;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     HPROF_START;
-    for (uint32_t s = lane; s < 256; s += 64) {
-        s_freq[s] = freq32[(size_t)b * 256 + s];
-        s_first[s] = first32[(size_t)b * 256 + s];
-        s_len[s] = 0;
-        s_code[s] = 0;
-    }
-    if (lane == 0) s_err = 0;
-    __syncthreads();
+    const uint32_t fq = freq32[(size_t)b * 256 + tid], fs = first32[(size_t)b * 256 + tid];
+    s_freq[tid] = fq;
+    s_len[tid] = 0;
+    s_code[tid] = 0;
     // leaves in first-occurrence order (main.cpp:238-244); first positions are distinct
-    uint32_t L = 0;
-    for (uint32_t s = lane; s < 256; s += 64) L += s_freq[s] > 0;
-    L = wave_sum_dpp(L);
-    for (uint32_t s = lane; s < 256; s += 64) s_lkey[s] = s_freq[s] ? s_first[s] : ~0ull;
-    __syncthreads();
-    {
-        uint32_t pos[4];
-        rank4_u64(s_lkey, lane, pos);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (s_freq[lane + 64 * k]) s_order[pos[k]] = (uint8_t)(lane + 64 * k);
+    s_lkey[tid] = fq ? fs : ~0ull;
+    if (tid == 0) {
+        s_err = 0;
+        s_bits = 0;
     }
+    const uint32_t L = (uint32_t)__syncthreads_count(fq > 0);
+    if (fq) s_order[rank_u64(s_lkey, fs)] = (uint8_t)tid;
     __syncthreads();
     if (L == 0) {
-        if (lane == 0) atomicOr(status, kStatusEmpty);
+        if (tid == 0) atomicOr(status, kStatusEmpty);
         return;
     }
     HPROF(0);  // loads, leaf count, leaf order
@@ -166,6 +163,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         if (rb != kModelOrder) ro = ridx[rb + L];
     }
     if (ro != kModelOrder) {
+      if (wave == 0) {
         // the internal nodes' ranks need not ascend, so the queue is simulated as it is: every
         // live node's key in a register slot (node v: lane v & 63, slot v >> 6), each pop a
         // wave-wide minimum (smallest frequency, then the larger address rank). The blocks here
@@ -212,6 +210,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
             for (uint32_t k = 0; k < 8; ++k)  // the owning lane builds the new node's key
                 if (lane + 64 * k == v) key[k] = (f << 9) | (511u - rkr[k]);
         }
+      }
     } else {
         // The reference's priority queue (main.cpp:245-254: first pop -> left child, second ->
         // right) in parallel rounds. A new node's frequency is the sum of the two it was made from,
@@ -228,17 +227,13 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         // remaining items as the heap would. Random data takes ~10 rounds, text and Calgary
         // 15-27, instead of L - 1 sequential merges (tests/test_huffman_queue.py restates it).
         // leaf keys (frequency, descending address rank, id), sorted into s_k1
-        for (uint32_t id = lane; id < 256; id += 64) s_lkey[id] = id < L ? heap_key(s_freq[s_order[id]], L, id) : ~0ull;
+        const uint64_t lk = tid < L ? heap_key(s_freq[s_order[tid]], L, tid) : ~0ull;
+        s_lkey[tid] = lk;
         __syncthreads();
-        {
-            uint32_t pos[4];
-            rank4_u64(s_lkey, lane, pos);
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (lane + 64 * k < L) s_k1[pos[k]] = s_lkey[lane + 64 * k];
-        }
+        if (tid < L) s_k1[rank_u64(s_lkey, lk)] = lk;
         __syncthreads();
         HPROF(5);  // (model path) leaf keys ranked
+      if (wave == 0) {
         uint64_t *s_P = s_q2;          // P (keys), 2 L - 2 entries
         uint64_t *s_IK = s_pcode;      // sorted internal keys (s_pcode is free until the codes)
         __shared__ uint32_t s_F[256];  // F[j]
@@ -288,7 +283,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
             }
             if (bound) {
                 for (uint32_t x = ic + lane; x < ia; x += 64) s_IK[x] = ikey(node_of(x));
-                __syncthreads();
+                WAVE_SYNC();
                 const uint32_t base = lc + ic;
                 for (uint32_t i = lc + lane; i < la; i += 64) {
                     const uint64_t key = s_k1[i];
@@ -313,7 +308,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                     else ++ic;
                 }
             }
-            __syncthreads();
+            WAVE_SYNC();
             const uint32_t m2 = min((lc + ic) / 2, L - 1);
             for (uint32_t j = m + lane; j < m2; j += 64) {
                 const uint64_t a = s_P[2 * j], c = s_P[2 * j + 1];
@@ -321,7 +316,7 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 s_right[L + j] = (int16_t)(c & 0xffffu);
                 s_F[j] = (uint32_t)(a >> 32) + (uint32_t)(c >> 32);
             }
-            __syncthreads();
+            WAVE_SYNC();
             m = m2;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -331,19 +326,20 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
                 gm[k] = __ballot(st);
             }
         }
+      }
     }
     __syncthreads();
     HPROF(1);  // the queue (merges; key ranking too on the heap-history path)
     // codes (left 0, right 1; a root leaf gets the empty code) by pointer jumping on parent
     // links: node x keeps (target a, path bits c, path length d) with code(x) = code(a) << d | c
     const uint32_t nn = 2 * L - 1;  // nodes; the root (nn - 1) is its own target
-    for (uint32_t v = lane; v < nn; v += 64) {
+    for (uint32_t v = tid; v < nn; v += kHuffThreads) {
         s_par[v] = (uint16_t)v;
         s_dep[v] = 0;
         s_pcode[v] = 0;
     }
     __syncthreads();
-    for (uint32_t v = L + lane; v < nn; v += 64) {
+    for (uint32_t v = L + tid; v < nn; v += kHuffThreads) {
         const uint32_t a = (uint32_t)s_left[v], c = (uint32_t)s_right[v];
         s_par[a] = (uint16_t)v;
         s_dep[a] = 1;
@@ -355,12 +351,12 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     // depth <= 255 < 2^9: at most 9 rounds; done as soon as every target is the root (a code
     // tree of depth D takes ceil(log2 D) rounds: ~5 for a 256-leaf tree)
     for (uint32_t round = 0; round < 9; ++round) {
-        uint32_t na[8], nd[8];
-        uint64_t nc[8];
+        uint32_t na[2], nd[2];
+        uint64_t nc[2];
         bool more = false;
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {  // all reads of the round before any write
-            const uint32_t v = lane + 64 * k;
+        for (uint32_t k = 0; k < 2; ++k) {  // all reads of the round before any write
+            const uint32_t v = tid + kHuffThreads * k;
             na[k] = v;
             nd[k] = 0;
             nc[k] = 0;
@@ -377,36 +373,36 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         }
         __syncthreads();
 #pragma unroll
-        for (uint32_t k = 0; k < 8; ++k) {
-            const uint32_t v = lane + 64 * k;
+        for (uint32_t k = 0; k < 2; ++k) {
+            const uint32_t v = tid + kHuffThreads * k;
             if (v < nn) {
                 s_par[v] = (uint16_t)na[k];
                 s_dep[v] = (uint16_t)min(nd[k], 0xffffu);
                 s_pcode[v] = nc[k];
             }
         }
-        __syncthreads();
-        if (!__any(more)) break;  // one wave: the exit is uniform
+        if (!__syncthreads_or(more)) break;  // the barrier of the writes; a uniform exit
     }
     HPROF(2);  // pointer jumping
     // leaves: code book, and the left-aligned codes, whose order is the preorder of the leaves
-    for (uint32_t v = lane; v < 256; v += 64) {
-        if (v >= L) {
-            s_lkey[v] = ~0ull;
-            continue;
-        }
-        const uint32_t d = s_dep[v], sym = s_order[v];
-        if (d > 64) atomicOr(&s_err, kStatusCodeLen);
-        const uint64_t code = d > 64 ? 0ull : s_pcode[v];
-        s_len[sym] = (uint8_t)min(d, 255u);
-        s_code[sym] = code;
-        s_lkey[v] = d == 0 ? 0ull : d > 64 ? ~0ull : code << (64 - d);
+    uint32_t dv = 0, symv = 0;
+    uint64_t lcode = ~0ull;  // this thread's leaf (v = tid < L): depth, symbol, left-aligned code
+    if (tid < L) {
+        dv = s_dep[tid];
+        symv = s_order[tid];
+        if (dv > 64) atomicOr(&s_err, kStatusCodeLen);
+        const uint64_t code = dv > 64 ? 0ull : s_pcode[tid];
+        s_len[symv] = (uint8_t)min(dv, 255u);
+        s_code[symv] = code;
+        lcode = dv == 0 ? 0ull : dv > 64 ? ~0ull : code << (64 - dv);
     }
+    s_lkey[tid] = lcode;
     // preorder tree bits (tree_to_bytes main.cpp:174-196): all 10L - 1 bits start as internal
     // '1's; leaf j in preorder (j leaves and depth + j - popcount(code) internal nodes before
     // it) owns bits [10j + depth - popcount, +9): a '0' then its 8 value bits MSB-first
     const uint32_t tbits = 10 * L - 1;
-    for (uint32_t w = lane; w < 80; w += 64) {
+    if (tid < 80) {
+        const uint32_t w = tid;
         uint32_t x = 0;
         for (uint32_t k = 0; k < 32; ++k) {
             const uint32_t bit = 32 * w + 8 * (k >> 3) + (7 - (k & 7));  // stream bit of u32 bit k
@@ -415,16 +411,11 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         s_tree32[w] = x;
     }
     __syncthreads();
-    uint32_t jpos[4];
-    rank4_u64(s_lkey, lane, jpos);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t v = lane + 64 * k, j = jpos[k];
-        if (v >= L) continue;
-        const uint32_t d = s_dep[v], sym = s_order[v];
-        const uint32_t off = 10 * j + min(d, 64u) - (uint32_t)__builtin_popcountll(s_pcode[v]);
+    if (tid < L) {
+        const uint32_t j = rank_u64(s_lkey, lcode);
+        const uint32_t off = 10 * j + min(dv, 64u) - (uint32_t)__builtin_popcountll(s_pcode[tid]);
         for (uint32_t i = 0; i < 9; ++i) {
-            const uint32_t one = i == 0 ? 0u : (sym >> (8 - i)) & 1u;
+            const uint32_t one = i == 0 ? 0u : (symv >> (8 - i)) & 1u;
             if (!one) {
                 const uint32_t pbit = off + i, byte = pbit >> 3;
                 atomicAnd(&s_tree32[byte >> 2], ~(1u << (8 * (byte & 3) + 7 - (pbit & 7))));
@@ -434,18 +425,17 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
     __syncthreads();
     DevTable *t = &tabs[b];
     HPROF(3);  // codes, preorder ranks, tree bits
-    uint64_t bits = 0;
-    for (uint32_t s = lane; s < 256; s += 64) {
-        t->code[s] = s_code[s];
-        t->len[s] = s_len[s];
-        bits += (uint64_t)s_freq[s] * s_len[s];
-    }
+    const uint32_t ln = s_len[tid];
+    t->code[tid] = s_code[tid];
+    t->len[tid] = (uint8_t)ln;
+    uint64_t bits = (uint64_t)s_freq[tid] * ln;
     for (int off = 32; off >= 1; off >>= 1) bits += __shfl_xor(bits, off, 64);
+    if (lane == 0) atomicAdd((unsigned long long *)&s_bits, (unsigned long long)bits);
     const uint32_t tree_len = (tbits + 7) >> 3;
     const uint64_t n = boffs[b + 1] - boffs[b];
     const uint32_t p = prim[b];
     uint8_t *h = hdr + (size_t)b * kHdrStride;
-    for (uint32_t i = lane; i < 24 + tree_len; i += 64) {
+    for (uint32_t i = tid; i < 24 + tree_len; i += kHuffThreads) {
         uint8_t v;
         if (i < 8) v = (uint8_t)((uint64_t)p >> (8 * i));
         else if (i < 16) v = (uint8_t)(n >> (8 * (i - 8)));
@@ -453,9 +443,10 @@ __global__ __launch_bounds__(64) void k_huff_build(const uint32_t *__restrict__ 
         else v = s_tree[i - 24];
         h[i] = v;
     }
-    if (lane == 0) {
+    __syncthreads();
+    if (tid == 0) {
         hdr_len[b] = 24 + tree_len;
-        const uint64_t pb = (bits + 7) / 8;
+        const uint64_t pb = (s_bits + 7) / 8;
         pay_bytes[b] = pb ? pb : 1;  // encode_with_huffman starts from one zero byte (main.cpp:162)
         uint32_t e = s_err;
         if (p == 0xffffffffu) e |= kStatusPrimary;
@@ -571,7 +562,7 @@ void codebook_batch(Ctx *c, const Batch &bt, const uint64_t *d_boffs, const uint
         d_ridx = d_rbase + nb;
         d_rrank = (const uint16_t *)(d_ridx + c->ws_aux[WS_BAND][1]);
     }
-    BMH_LAUNCH(c, "huff_build", k_huff_build, nb, 64, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
+    BMH_LAUNCH(c, "huff_build", k_huff_build, nb, kHuffThreads, 0, d_freq, d_first, d_prim, d_boffs, d_tabs, d_hdr, d_hlen, d_payb,
                d_status, d_rbase, d_ridx, d_rrank);
 #ifdef BMH_PROF_HUFF
     {
