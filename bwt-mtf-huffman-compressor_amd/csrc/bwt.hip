@@ -487,11 +487,13 @@ __device__ uint32_t g_dprof[(1u << 18) * 8];
 #define DPROF_START
 #endif
 
-// 1024 threads x 16 positions a chunk. recount = 0 (grid = the chunk list): raw 10-bit digits
+// 512 threads x 32 positions a chunk (two 16-byte loads a thread: twice the bytes in flight of
+// one, at the same four workgroups' worth of waves a CU). recount = 0 (grid = the chunk list): raw 10-bit digits
 // for every block, plus the census (bits); recount = 1 (a grid of <= 2048 striding over rlist,
 // the chunks of compacted blocks k_g1_census_fin listed): those chunks' digits by the block's
 // alphabet (ainfo / arank) — on a batch with none, a few thousand workgroups read a zero count.
-__global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
+constexpr uint32_t kG1HistNT = 512;
+__global__ __launch_bounds__(kG1HistNT) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ rlist,
                                                   uint32_t *__restrict__ chist, const uint32_t *__restrict__ ainfo,
                                                   const uint8_t *__restrict__ arank, uint32_t *__restrict__ bits,
@@ -512,30 +514,39 @@ __global__ __launch_bounds__(1024) void k_g1_hist(const uint8_t *__restrict__ da
         }
         const uint32_t info = recount ? ainfo[ch.block] : 0u;
         __syncthreads();                 // the previous chunk's reads of h / s_rk
-        for (uint32_t i = t; i < 4 * kG1Bins; i += 1024) (&h[0][0])[i] = 0;
+        for (uint32_t i = t; i < 4 * kG1Bins; i += kG1HistNT) (&h[0][0])[i] = 0;
         if (info && t < 256) s_rk[t] = arank[(size_t)ch.block * 256 + t];
         __syncthreads();
-        const uint32_t boff = boffs[ch.block], n = boffs[ch.block + 1] - boff;
-        const uint8_t *blk = data + boff;
-        const uint32_t e = 16 * t;
+        // the block's offset and length ride in the chunk entry (no dependent load of boffs)
+        const uint32_t n = ch.n;
+        const uint8_t *blk = data + ch.boff;
+        const uint32_t e = 32 * t;
         if (e < ch.len) {
-            uint32_t dg[4];
+            uint32_t dg[4], dgb[4];  // the thread's run [e, e + nv): pieces A and B
             g1_load16(blk, ch.start, ch.len, e, dg);
-            const uint32_t nv = min(16u, ch.len - e);
-            // the two bytes after the run (cyclic; n may be 1 or 2)
-            const uint32_t ni = (ch.start + e + nv) % n, ni2 = (ni + 1) % n;
+            g1_load16(blk, ch.start, ch.len, e + 16, dgb);
+            const uint32_t nv = min(32u, ch.len - e);
+            // the two bytes after the run (cyclic; n may be 1 or 2): start + e + nv <= n
+            const uint32_t x = ch.start + e + nv, ni = x >= n ? x - n : x, ni2 = ni + 1 >= n ? ni + 1 - n : ni + 1;
             const uint32_t nx = blk[ni], nx2 = blk[ni2];
-            if (nv == 16) {
+            if (nv == 32) {
 #pragma unroll
-                for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dg, k, 16, nx, nx2, info, s_rk)], 1u);
+                for (uint32_t k = 0; k < 16; ++k)
+                    atomicAdd(&h[w][g1_digit(dg, k, 16, byte_of(dgb, 0), byte_of(dgb, 1), info, s_rk)], 1u);
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) atomicAdd(&h[w][g1_digit(dgb, k, 16, nx, nx2, info, s_rk)], 1u);
             } else {
-                for (uint32_t k = 0; k < nv; ++k) atomicAdd(&h[w][g1_digit(dg, k, nv, nx, nx2, info, s_rk)], 1u);
+                // piece A's following bytes: B's first two while inside the run, then the run's
+                const uint32_t nva = min(16u, nv);
+                const uint32_t a1 = nv > 16 ? byte_of(dgb, 0) : nx;
+                const uint32_t a2 = nv > 17 ? byte_of(dgb, 1) : nv == 17 ? nx : nx2;
+                for (uint32_t k = 0; k < nva; ++k) atomicAdd(&h[w][g1_digit(dg, k, nva, a1, a2, info, s_rk)], 1u);
+                for (uint32_t k = 0; k + 16 < nv; ++k) atomicAdd(&h[w][g1_digit(dgb, k, nv - 16, nx, nx2, info, s_rk)], 1u);
             }
         }
         __syncthreads();
-        static_assert(kG1Bins == 1024, "one digit a thread");
-        const uint32_t sum = h[0][t] + h[1][t] + h[2][t] + h[3][t];
-        chist[(size_t)ci * kG1Bins + t] = sum;
+        static_assert(kG1Bins == 2 * kG1HistNT, "two digits a thread");
+        for (uint32_t d = t; d < kG1Bins; d += kG1HistNT) chist[(size_t)ci * kG1Bins + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
         if (!recount) {
             // the chunk's bytes: byte v is present iff one of the digits 4v .. 4v + 3 is counted
             // (read from the four waves' partial counts: no further barrier)
@@ -663,7 +674,7 @@ __global__ __launch_bounds__(1024) void k_g1_scatter(DataArgs a, const GChunk *_
     if (ch.len == 0) return;
     GPROF_START;
     const uint32_t t = threadIdx.x;
-    const uint32_t b = ch.block, boff = a.boffs[b], n = a.boffs[b + 1] - boff;
+    const uint32_t b = ch.block, boff = ch.boff, n = ch.n;  // (carried by the chunk entry: no dependent load)
     const uint32_t info = a.ainfo[b], db = g1_db(info);
     // packed records for a compacted block's dense buckets (nsym symbols of wsym bits; 0: raw)
     const uint32_t nsym = info ? rec_nsym(info, min(32u, 44u - rec_pbits(n))) : 0u, wsym = g1_w(info);
@@ -2553,11 +2564,11 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             // ---- data phase
             // raw digits + each block's byte census, the blocks' alphabets, then the chunks of
             // compacted blocks recounted
-            BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, 1024, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo,
+            BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, kG1HistNT, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo,
                        arank, abits, 0u);
             BMH_LAUNCH(c, "bwt_g1_census", k_g1_census_fin, nb, 256, 0, abits, d_bchunks, d_bchunk0, ainfo, arank,
                        rlist);
-            BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), 1024, 0, d_in, d_boffs,
+            BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), kG1HistNT, 0, d_in, d_boffs,
                        d_chunks, rlist, chist, ainfo, arank, abits, 1u);
             BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_sum, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, chist,
                        g1part);

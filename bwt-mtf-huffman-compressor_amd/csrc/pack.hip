@@ -85,7 +85,10 @@ constexpr uint32_t kPackImgWords = 2048;
 // Consecutive chunks per workgroup: the code table is loaded once per block run, the next
 // chunk's symbols are in flight while this one is packed, and the image is zeroed by the
 // store pass that drains it (no zeroing pass and barrier per chunk).
-constexpr uint32_t kPackCPW = 4;  // 2 / 8 measured no faster
+#ifndef BMH_PACK_CPW
+#define BMH_PACK_CPW 16
+#endif
+constexpr uint32_t kPackCPW = BMH_PACK_CPW;  // 4 -> 8 -> 16: 0.81 -> 0.75 -> 0.71 ms per GiB (round 6)
 
 __device__ __forceinline__ uint4 pack_load_syms(const uint8_t *__restrict__ mtf, const PChunk &ch, uint32_t t)
 {
@@ -101,6 +104,36 @@ __device__ __forceinline__ uint4 pack_load_syms(const uint8_t *__restrict__ mtf,
     return v4;
 }
 
+// LDS slot of image word w: one pad word per 64, so lanes whose words are 4 apart (8-bit codes,
+// 16 symbols a thread) or 2 apart fall in distinct banks
+__device__ __forceinline__ uint32_t img_at(uint32_t w)
+{
+#ifdef BMH_PACK_SWZ
+    return w + (w >> 6);
+#else
+    return w;
+#endif
+}
+
+// Bits [0, l) of a code word, left-aligned in a 32-bit word, appended MSB-first to the 64-bit
+// accumulator (hi, lo) holding nacc < 32 bits; a completed word is OR'd into the image
+// (kWin: only words inside the window [wb, wb + nw)).
+template <bool kWin>
+__device__ __forceinline__ void pack_push(uint32_t v, uint32_t l, uint32_t &hi, uint32_t &lo, uint32_t &nacc, uint32_t &w,
+                                          uint32_t *s_img, uint32_t wb, uint32_t nw)
+{
+    hi |= v >> nacc;                                // (v : 0) >> nacc, high word
+    lo |= __builtin_amdgcn_alignbit(v, 0u, nacc);  // and low word
+    nacc += l;
+    if (nacc >= 32) {
+        if (!kWin || w - wb < nw) atomicOr(&s_img[img_at(w - wb)], hi);
+        hi = lo;
+        lo = 0;
+        ++w;
+        nacc -= 32;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ mtf, const PChunk *__restrict__ chunks,
                                                     uint32_t nch, const DevTable *__restrict__ tabs,
                                                     const uint64_t *__restrict__ cboff,
@@ -108,16 +141,37 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
                                                     const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ out,
                                                     const uint32_t *status)
 {
-    __shared__ uint64_t s_tab[256];  // code << 8 | length (lengths <= 56)
+    // code word left-aligned in 64 bits, its length in the low 8 bits (lengths <= 56, so the
+    // code's last bit is above bit 8): the high half is the whole code whenever it fits 32 bits
+    __shared__ uint64_t s_tab[256];
     __shared__ uint32_t s_tmp[8];
-    __shared__ uint32_t s_img[kPackImgWords];
-    if (status && (*status & kStatusCapacity)) return;
+    __shared__ uint32_t s_img[kPackImgWords + kPackImgWords / 64];
+    // per chunk of the workgroup, fetched up front (no dependent global loads per chunk): its first
+    // bit, its block's first payload bit and bit offset within the block; whether it is the block's last
+    __shared__ uint64_t s_G[kPackCPW], s_P[kPackCPW], s_cb[kPackCPW];
+    __shared__ uint32_t s_last[kPackCPW];
+    // the loads of the start are issued together (the status word, the chunk's symbols, its code
+    // book and the per-chunk offsets), then waited for once
+    const uint32_t st = status ? *status : 0u;
     const uint32_t t = threadIdx.x;
     const uint32_t c0 = blockIdx.x * kPackCPW, c1 = min(c0 + kPackCPW, nch);
-    for (uint32_t w = t; w < kPackImgWords; w += 256) s_img[w] = 0;
-    uint32_t tblock = ~0u;
     PChunk ch = chunks[c0];
     uint4 v4 = pack_load_syms(mtf, ch, t);  // this chunk's 16 symbols of the thread
+    uint32_t tl = tabs[ch.block].len[t];
+    uint64_t tc = tabs[ch.block].code[t];
+    if (t < c1 - c0) {
+        const uint32_t c = c0 + t, b = chunks[c].block;
+        const uint64_t P = pay_offs[b] * 8, cb = cboff[c];
+        s_P[t] = P;
+        s_cb[t] = cb;
+        s_G[t] = P + cb;
+        s_last[t] = c + 1 == cfirst[b + 1];
+    }
+    if (st & kStatusCapacity) return;  // workgroup-uniform
+    for (uint32_t w = t; w < kPackImgWords + kPackImgWords / 64; w += 256) s_img[w] = 0;
+    uint32_t tblock = ~0u;
+    bool long32 = false;  // the block's code book has words longer than 32 bits (workgroup-uniform)
+    bool short16 = false;  // all its words are <= 16 bits: two per push
     for (uint32_t c = c0; c < c1; ++c) {
         // the next chunk's symbols are loaded while this one is packed
         PChunk nx = ch;
@@ -127,94 +181,97 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
             nv4 = pack_load_syms(mtf, nx, t);
         }
         if (ch.block != tblock) {  // workgroup-uniform; the previous chunk's readers are past a barrier
-            const DevTable *tb_ = &tabs[ch.block];
-            s_tab[t] = (tb_->code[t] << 8) | tb_->len[t];
+            if (tblock != ~0u) {  // a later block of the workgroup's chunks
+                tl = tabs[ch.block].len[t];
+                tc = tabs[ch.block].code[t];
+            }
+            const uint32_t l = tl;
+            s_tab[t] = l ? (tc << (64 - l)) | l : 0ull;
             tblock = ch.block;
-            __syncthreads();
+            const int lx = __syncthreads_or(l > 16) | (__syncthreads_or(l > 32) << 1);
+            short16 = lx == 0;
+            long32 = lx > 1;
         }
         const uint32_t i0 = t * kPackIPT;
         const uint32_t nsym = i0 < ch.len ? min(kPackIPT, ch.len - i0) : 0u;
-        const uint64_t P = pay_offs[ch.block] * 8;  // the block's first payload bit
-        const uint64_t G = P + cboff[c];            // this chunk's first bit
+        // (s_G .. s_last were written before the first chunk's code book barrier)
+        const uint64_t P = s_P[c - c0];  // the block's first payload bit
+        const uint64_t G = s_G[c - c0];  // this chunk's first bit
         const uint64_t W0 = G >> 5;
         const uint32_t sh0 = (uint32_t)(G & 31u);
         const uint32_t *vw = &v4.x;
+        // the thread's code word k (0 past the chunk's end)
+        auto code = [&](uint32_t k) -> uint64_t { return k < nsym ? s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] : 0ull; };
         uint32_t mybits = 0;  // a chunk holds at most 4096 * 56 bits
+        uint32_t hw[kPackIPT], ll[kPackIPT];  // code words' high halves; lengths
 #pragma unroll
-        for (uint32_t k = 0; k < kPackIPT; ++k)
-            if (k < nsym) mybits += (uint32_t)s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] & 255u;
+        for (uint32_t k = 0; k < kPackIPT; ++k) {
+            const uint64_t ek = code(k);
+            hw[k] = (uint32_t)(ek >> 32);
+            ll[k] = (uint32_t)ek & 255u;
+            mybits += ll[k];
+        }
         uint32_t total32;
         const uint32_t tb = block_excl_sum1<256>(mybits, s_tmp, &total32) + sh0;  // bit offset from W0 * 32
         // the block's last chunk also owns the zero pad bits up to the payload's last byte
         // (at least one byte: encode_with_huffman starts from one zero byte, main.cpp:162)
-        const bool last = c + 1 == cfirst[ch.block + 1];
+        const bool last = s_last[c - c0] != 0;
         uint64_t own_end = G + total32;
         if (last) {
-            const uint64_t bbits = cboff[c] + total32;
+            const uint64_t bbits = s_cb[c - c0] + total32;
             const uint64_t pb = (bbits + 7) / 8;
             own_end = P + 8 * (pb ? pb : 1);
         }
         const uint32_t nwords = own_end == G ? 0u : (uint32_t)((own_end - W0 * 32 + 31) >> 5);
         for (uint32_t wb = 0; wb < nwords; wb += kPackImgWords) {
             const uint32_t nw = min(kPackImgWords, nwords - wb);
-            if (nsym && (tb >> 5) < wb + nw && ((tb + mybits + 31) >> 5) > wb) {
-                // this thread's bits [tb, tb + mybits) accumulated MSB-first in a 64-bit register,
-                // flushed a word at a time: the first word may be shared with the previous thread
-                // (LDS atomicOr), words outside the window are dropped
-                uint32_t w = tb >> 5, nacc = tb & 31u;
-                const uint32_t w_head = w;
-                const bool head_shared = nacc != 0;
-                uint64_t acc = 0;
-                auto flush = [&](uint32_t word) {
-                    const uint32_t wi = w - wb;
-                    if (wi < nw) {
-                        if (w == w_head && head_shared) atomicOr(&s_img[wi], word);
-                        else s_img[wi] = word;
-                    }
-                    ++w;
-                };
-                auto push = [&](uint32_t v, uint32_t l) {  // 1 <= l <= 32 bits, MSB-first
-                    acc |= ((uint64_t)v << (64 - l)) >> nacc;
-                    nacc += l;
-                    if (nacc >= 32) {
-                        flush((uint32_t)(acc >> 32));
-                        acc <<= 32;
-                        nacc -= 32;
-                    }
-                };
+            // this thread's bits [tb, tb + mybits) accumulated MSB-first in 64 bits and OR'd into
+            // the image a word at a time (the first and last words may be shared with the
+            // neighbouring threads); words outside the window are dropped
+            if (mybits && (tb >> 5) < wb + nw && ((tb + mybits + 31) >> 5) > wb) {
+                uint32_t w = tb >> 5, nacc = tb & 31u, hi = 0, lo = 0;
+                if (short16 && nwords <= kPackImgWords) {
+                    // one window (wb = 0); two words of <= 16 bits joined per push (padding words
+                    // are empty: no bits)
 #pragma unroll
-                for (uint32_t k = 0; k < kPackIPT; ++k) {
-                    const uint64_t e = k < nsym ? s_tab[(vw[k >> 2] >> (8 * (k & 3))) & 255u] : 0ull;
-                    const uint32_t l = (uint32_t)e & 255u;
-                    const uint64_t code = e >> 8;
-                    if (l > 32) {  // codes longer than 32 bits (never on 8-bit alphabets in practice)
-                        push((uint32_t)(code >> 32), l - 32);
-                        push((uint32_t)code, 32);
-                    } else if (l) {
-                        push((uint32_t)code, l);
+                    for (uint32_t k = 0; k < kPackIPT; k += 2)
+                        pack_push<false>(hw[k] | (hw[k + 1] >> ll[k]), ll[k] + ll[k + 1], hi, lo, nacc, w, s_img, 0u, nw);
+                } else if (!long32 && nwords <= kPackImgWords) {
+                    // one window, one push per symbol
+#pragma unroll
+                    for (uint32_t k = 0; k < kPackIPT; ++k) pack_push<false>(hw[k], ll[k], hi, lo, nacc, w, s_img, 0u, nw);
+                } else {
+#pragma unroll
+                    for (uint32_t k = 0; k < kPackIPT; ++k) {
+                        const uint64_t ek = code(k);
+                        const uint32_t l = (uint32_t)ek & 255u;
+                        pack_push<true>((uint32_t)(ek >> 32), min(l, 32u), hi, lo, nacc, w, s_img, wb, nw);
+                        if (l > 32) pack_push<true>((uint32_t)ek & ~255u, l - 32, hi, lo, nacc, w, s_img, wb, nw);
                     }
                 }
-                if (nacc) {
-                    const uint32_t wi = w - wb;
-                    if (wi < nw) atomicOr(&s_img[wi], (uint32_t)(acc >> 32));
-                }
+                if (nacc && w - wb < nw) atomicOr(&s_img[img_at(w - wb)], hi);
             }
             __syncthreads();
             // words wholly inside [G, own_end) are stored; the edge words are shared with the
             // neighbouring chunks / record headers: only this chunk's bits are replaced,
             // atomically. Each word is zeroed as it is drained (the next window starts clean).
+            uint32_t *ob = out + (W0 + wb);
             for (uint32_t w = t; w < nw; w += 256) {
+                const uint32_t slot = img_at(w), v = __builtin_bswap32(s_img[slot]);
+                s_img[slot] = 0;
+                if (wb + w != 0 && wb + w + 1 != nwords) {  // interior words: whole
+                    ob[w] = v;
+                    continue;
+                }
                 const uint64_t ws = (W0 + wb + w) * 32;
                 const uint32_t a = G > ws ? (uint32_t)(G - ws) : 0u;
-                const uint32_t e = own_end < ws + 32 ? (uint32_t)(own_end - ws) : 32u;
-                const uint32_t v = __builtin_bswap32(s_img[w]);
-                s_img[w] = 0;
-                if (a == 0 && e == 32) {
-                    out[W0 + wb + w] = v;
+                const uint32_t e2 = own_end < ws + 32 ? (uint32_t)(own_end - ws) : 32u;
+                if (a == 0 && e2 == 32) {
+                    ob[w] = v;
                 } else {
-                    const uint32_t m = __builtin_bswap32((0xffffffffu >> a) & (0xffffffffu << (32 - e)));
-                    atomicAnd(&out[W0 + wb + w], ~m);
-                    atomicOr(&out[W0 + wb + w], v & m);
+                    const uint32_t m = __builtin_bswap32((0xffffffffu >> a) & (0xffffffffu << (32 - e2)));
+                    atomicAnd(&ob[w], ~m);
+                    atomicOr(&ob[w], v & m);
                 }
             }
             __syncthreads();
