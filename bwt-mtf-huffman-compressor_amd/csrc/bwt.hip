@@ -495,7 +495,7 @@ __device__ uint32_t g_dprof[(1u << 18) * 8];
 constexpr uint32_t kG1HistNT = 512;
 __global__ __launch_bounds__(kG1HistNT) void k_g1_hist(const uint8_t *__restrict__ data, const uint32_t *__restrict__ boffs,
                                                   const GChunk *__restrict__ chunks, uint32_t *__restrict__ rlist,
-                                                  uint32_t *__restrict__ chist, const uint32_t *__restrict__ ainfo,
+                                                  uint16_t *__restrict__ ccnt, const uint32_t *__restrict__ ainfo,
                                                   const uint8_t *__restrict__ arank, uint32_t *__restrict__ bits,
                                                   uint32_t recount)  // bits: 8 words a chunk
 {
@@ -545,8 +545,14 @@ __global__ __launch_bounds__(kG1HistNT) void k_g1_hist(const uint8_t *__restrict
             }
         }
         __syncthreads();
-        static_assert(kG1Bins == 2 * kG1HistNT, "two digits a thread");
-        for (uint32_t d = t; d < kG1Bins; d += kG1HistNT) chist[(size_t)ci * kG1Bins + d] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+        // u16 counts (a chunk holds <= 16 K rotations), two adjacent digits a thread
+        static_assert(kG1Chunk <= 65535 && kG1Bins == 2 * kG1HistNT, "u16 digit counts, two a thread");
+        {
+            const uint32_t d = 2 * t;
+            const uint32_t lo = h[0][d] + h[1][d] + h[2][d] + h[3][d];
+            const uint32_t hi = h[0][d + 1] + h[1][d + 1] + h[2][d + 1] + h[3][d + 1];
+            ((uint32_t *)ccnt)[(size_t)ci * (kG1Bins / 2) + t] = lo | (hi << 16);
+        }
         if (!recount) {
             // the chunk's bytes: byte v is present iff one of the digits 4v .. 4v + 3 is counted
             // (read from the four waves' partial counts: no further barrier)
@@ -575,7 +581,7 @@ __global__ __launch_bounds__(kG1HistNT) void k_g1_hist(const uint8_t *__restrict
 constexpr uint32_t kG1ScanParts = 4;
 __global__ __launch_bounds__(kG1Bins) void k_g1_scan_sum(const uint32_t *__restrict__ bchunks,
                                                          const uint32_t *__restrict__ bchunk0,
-                                                         const uint32_t *__restrict__ chist, uint32_t *__restrict__ part)
+                                                         const uint16_t *__restrict__ ccnt, uint32_t *__restrict__ part)
 {
     const uint32_t b = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
     const uint32_t c0 = bchunk0[b], nc = bchunks[b], nq = (nc + kG1ScanParts - 1) / kG1ScanParts;
@@ -585,7 +591,7 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan_sum(const uint32_t *__restr
     for (uint32_t k = k0; k < k1; k += U) {
         uint32_t v[U];
 #pragma unroll
-        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? chist[(size_t)(c0 + 8 * (k + j)) * kG1Bins + d] : 0u;
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? ccnt[(size_t)(c0 + 8 * (k + j)) * kG1Bins + d] : 0u;
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j) run += v[j];
     }
@@ -632,23 +638,25 @@ __global__ __launch_bounds__(kG1Bins) void k_g1_scan(const uint32_t *__restrict_
 // grid (nblocks, kG1ScanParts): per-chunk write offsets (block-relative, in place over the
 // chunk counts), part q from its first offset
 __global__ __launch_bounds__(kG1Bins) void k_g1_scan_offs(const uint32_t *__restrict__ bchunks,
-                                                          const uint32_t *__restrict__ bchunk0, uint32_t *__restrict__ chist,
+                                                          const uint32_t *__restrict__ bchunk0,
+                                                          const uint16_t *__restrict__ ccnt, uint32_t *__restrict__ chist,
                                                           const uint32_t *__restrict__ part)
 {
     const uint32_t b = blockIdx.x, q = blockIdx.y, d = threadIdx.x;
     const uint32_t c0 = bchunk0[b], nc = bchunks[b], nq = (nc + kG1ScanParts - 1) / kG1ScanParts;
     const uint32_t k0 = q * nq, k1 = min(nc, k0 + nq);
     constexpr uint32_t U = 32;
-    auto at = [&](uint32_t k) -> uint32_t & { return chist[(size_t)(c0 + 8 * k) * kG1Bins + d]; };
+    // counts (u16) in, write offsets (u32) out
+    auto idx = [&](uint32_t k) -> size_t { return (size_t)(c0 + 8 * k) * kG1Bins + d; };
     uint32_t acc = part[((size_t)b * kG1ScanParts + q) * kG1Bins + d];
     for (uint32_t k = k0; k < k1; k += U) {
         uint32_t v[U];
 #pragma unroll
-        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? at(k + j) : 0u;
+        for (uint32_t j = 0; j < U; ++j) v[j] = k + j < k1 ? ccnt[idx(k + j)] : 0u;
 #pragma unroll
         for (uint32_t j = 0; j < U; ++j)
             if (k + j < k1) {
-                at(k + j) = acc;
+                chist[idx(k + j)] = acc;
                 acc += v[j];
             }
     }
@@ -2481,7 +2489,9 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
     uint32_t *sa = (uint32_t *)c->get(WS_SA, N * 4);
     uint32_t *sa2 = (uint32_t *)c->get(WS_SA2, N * 4);
     uint64_t *rec = (uint64_t *)c->get(WS_KEY8, N * 8);
-    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 4);
+    // chunk write offsets (u32, the scatter's) | chunk digit counts (u16)
+    uint32_t *chist = (uint32_t *)c->get(WS_CHIST, (size_t)nchunks * kG1Bins * 6);
+    uint16_t *ccnt = (uint16_t *)(chist + (size_t)nchunks * kG1Bins);
     // per-chunk byte sets (8 words a chunk) | per-block alphabet info | rank maps
     // | recount list length + chunk list
     uint8_t *d_alpha = (uint8_t *)c->get(WS_ALPHA, (size_t)nchunks * 36 + (size_t)nb * (4 + 256) + 64);
@@ -2564,18 +2574,18 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
             // ---- data phase
             // raw digits + each block's byte census, the blocks' alphabets, then the chunks of
             // compacted blocks recounted
-            BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, kG1HistNT, 0, d_in, d_boffs, d_chunks, rlist, chist, ainfo,
+            BMH_LAUNCH(c, "bwt_g1_hist", k_g1_hist, nchunks, kG1HistNT, 0, d_in, d_boffs, d_chunks, rlist, ccnt, ainfo,
                        arank, abits, 0u);
             BMH_LAUNCH(c, "bwt_g1_census", k_g1_census_fin, nb, 256, 0, abits, d_bchunks, d_bchunk0, ainfo, arank,
                        rlist);
             BMH_LAUNCH(c, "bwt_g1_hist2", k_g1_hist, std::min<uint32_t>(nchunks, 2048), kG1HistNT, 0, d_in, d_boffs,
-                       d_chunks, rlist, chist, ainfo, arank, abits, 1u);
-            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_sum, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, chist,
+                       d_chunks, rlist, ccnt, ainfo, arank, abits, 1u);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_sum, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, ccnt,
                        g1part);
             BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan, nb, kG1Bins, 0, d_boffs, g1part, bk, lb[0], lg[0], d_cnt, d_loff,
                        big_cap, ainfo);
-            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_offs, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, chist,
-                       g1part);
+            BMH_LAUNCH(c, "bwt_g1_scan", k_g1_scan_offs, dim3(nb, kG1ScanParts), kG1Bins, 0, d_bchunks, d_bchunk0, ccnt,
+                       chist, g1part);
         }
         pre_done = false;
         if (prologue_only) {

@@ -43,20 +43,32 @@ __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ m
     if (threadIdx.x == 0) cbits[blockIdx.x] = total;
 }
 
-// Chunk bit counts from the per-chunk MTF histograms: one wave per chunk, sum cnt[v] * len[v].
+// Chunk bit counts from the per-chunk MTF histograms, sum cnt[v] * len[v]: one wave per
+// kBitsCPW consecutive chunks, every histogram and chunk entry loaded before the first code-length
+// read (which depends on the chunk's block), so a wave waits for two loads, not two per chunk.
+constexpr uint32_t kBitsCPW = 4;
 __global__ __launch_bounds__(256) void k_pack_bits_hist(const uint16_t *__restrict__ chist,
                                                         const PChunk *__restrict__ chunks, uint32_t nch,
                                                         const DevTable *__restrict__ tabs, uint64_t *__restrict__ cbits)
 {
-    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63u;
-    if (c >= nch) return;
-    const DevTable *t = &tabs[chunks[c].block];
-    const uint2 h = *(const uint2 *)(chist + (size_t)c * 256 + 4 * l);
-    const uint32_t lw = *(const uint32_t *)(t->len + 4 * l);
-    uint64_t s = (uint64_t)(h.x & 0xffffu) * (lw & 255u) + (uint64_t)(h.x >> 16) * ((lw >> 8) & 255u) +
-                 (uint64_t)(h.y & 0xffffu) * ((lw >> 16) & 255u) + (uint64_t)(h.y >> 16) * (lw >> 24);
-    s = wave_sum64(s);
-    if (l == 0) cbits[c] = s;
+    const uint32_t c0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * kBitsCPW, l = threadIdx.x & 63u;
+    if (c0 >= nch) return;
+    uint2 h[kBitsCPW];
+    uint32_t blk[kBitsCPW];
+#pragma unroll
+    for (uint32_t i = 0; i < kBitsCPW; ++i) {
+        const uint32_t c = min(c0 + i, nch - 1);
+        h[i] = *(const uint2 *)(chist + (size_t)c * 256 + 4 * l);
+        blk[i] = chunks[c].block;
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kBitsCPW; ++i) {
+        const uint32_t lw = *(const uint32_t *)(tabs[blk[i]].len + 4 * l);
+        uint64_t s = (uint64_t)(h[i].x & 0xffffu) * (lw & 255u) + (uint64_t)(h[i].x >> 16) * ((lw >> 8) & 255u) +
+                     (uint64_t)(h[i].y & 0xffffu) * ((lw >> 16) & 255u) + (uint64_t)(h[i].y >> 16) * (lw >> 24);
+        s = wave_sum64(s);
+        if (l == 0 && c0 + i < nch) cbits[c0 + i] = s;
+    }
 }
 
 // grid = nblocks; exclusive scan of the block's chunk bit counts (in place); btot (may be null)
@@ -394,7 +406,7 @@ uint64_t *pack_bits_scan(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const Pa
 {
     uint64_t *d_cbits = (uint64_t *)c->get(WS_PACK_BITS, (size_t)pl.nch * 8);
     if (d_chist)
-        BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(pl.nch, 4), 256, 0, d_chist, pl.chunks, pl.nch, d_tabs,
+        BMH_LAUNCH(c, "pack_bits", k_pack_bits_hist, cdiv(pl.nch, 4 * kBitsCPW), 256, 0, d_chist, pl.chunks, pl.nch, d_tabs,
                    d_cbits);
     else
         BMH_LAUNCH(c, "pack_bits", k_pack_bits, pl.nch, 256, 0, d_mtf, pl.chunks, d_tabs, d_cbits);
