@@ -1101,3 +1101,29 @@ def test_speculative_round_with_run_heavy_block(ctx, oracle):
         else:
             assert hashlib.sha256(r).hexdigest() == man[g]["sha256"], i
             g += 1
+
+
+def test_text_batch_device_memory_stays_flat():
+    """a 128 MiB text batch (not dense: the multi-pipeline path on sub-contexts) must
+    not make the parent context also hold the dense prologue's BWT workspaces (~40 bytes per
+    input byte), and a second batch of the same layout allocates nothing more."""
+    torch = pytest.importorskip("torch")
+    c = bmh.Context(0)  # fresh: no dense batch of this layout before
+    n, bs = 128 << 20, 4 << 20
+    d_in = c.alloc(n)
+    c.synth_zipf(d_in, n, 0)
+    offs = np.arange(0, n + 1, bs, dtype=np.uint64)
+    cap = int(sum(bmh.lib().bmh_record_bound(bs) for _ in range(n // bs)))
+    d_out = c.alloc(cap)
+    free0, _ = torch.cuda.mem_get_info(0)
+    ro1 = c.encode_blocks_dev(d_in, offs, d_out, cap)
+    assert c.last_pipelines() > 1  # the text path: sub-contexts, not the dense single pipeline
+    free1, _ = torch.cuda.mem_get_info(0)
+    ro2 = c.encode_blocks_dev(d_in, offs, d_out, cap)
+    free2, _ = torch.cuda.mem_get_info(0)
+    assert np.array_equal(ro1, ro2)
+    grew = free0 - free1
+    print(f"text batch: {grew / n:.1f} B of device memory per input byte, then {(free1 - free2) >> 20} MiB")
+    assert grew <= 56 * n, f"first text batch took {grew / n:.1f} bytes of device memory per input byte"
+    assert free1 - free2 <= 64 << 20, f"second batch of the same layout allocated {(free1 - free2) >> 20} MiB"
+    del c
