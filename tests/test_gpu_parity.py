@@ -1124,6 +1124,8 @@ def test_text_batch_device_memory_stays_flat():
     assert np.array_equal(ro1, ro2)
     grew = free0 - free1
     print(f"text batch: {grew / n:.1f} B of device memory per input byte, then {(free1 - free2) >> 20} MiB")
-    assert grew <= 56 * n, f"first text batch took {grew / n:.1f} bytes of device memory per input byte"
+    # the sub-contexts' own workspaces measure ~60 B a byte; the parent's unused dense prologue
+    # would add ~40 more
+    assert grew <= 72 * n, f"first text batch took {grew / n:.1f} bytes of device memory per input byte"
     assert free1 - free2 <= 64 << 20, f"second batch of the same layout allocated {(free1 - free2) >> 20} MiB"
     del c
