@@ -79,6 +79,31 @@ static uint32_t mtf_chunk_len(Ctx *c, const Batch &bt)
 }
 constexpr int kLanes = 64;            // lanes (chunks) per encode workgroup (one wave)
 
+// Bytes [src, src + nv) (nv <= 64) into sw[16], zero past nv, from the 17 aligned dwords that
+// cover them: every load in flight at once (a byte loop waits for each load in turn), the bytes
+// funnel-shifted out; a dword past the last byte is read byte by byte (no read past the end).
+__device__ __forceinline__ void load64_any(const uint8_t *src, uint32_t nv, uint32_t (&sw)[16])
+{
+    const uintptr_t p0 = (uintptr_t)src, pa = p0 & ~(uintptr_t)3, end = p0 + nv;
+    const uint32_t sh = 8u * (uint32_t)(p0 & 3u);
+    uint32_t dw[17];
+#pragma unroll
+    for (uint32_t q = 0; q < 17; ++q) {
+        const uintptr_t qa = pa + 4 * q;
+        uint32_t x = 0;
+        if (qa + 4 <= end) {
+            x = *(const uint32_t *)qa;
+        } else if (qa < end) {
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k)
+                if (qa + k < end) x |= (uint32_t)((const uint8_t *)qa)[k] << (8 * k);
+        }
+        dw[q] = x;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 16; ++q) sw[q] = (uint32_t)(((uint64_t)dw[q + 1] << 32 | dw[q]) >> sh);
+}
+
 struct MChunk {
     uint32_t block, start, len, rel;  // rel = start - block offset
 };
@@ -132,12 +157,7 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
                 if (q == (k >> 2)) sw[q] |= x;
         }
     } else {
-        for (uint32_t k = 0; k < nv; ++k) {
-            const uint32_t x = (uint32_t)src[k] << (8 * (k & 3));
-#pragma unroll
-            for (uint32_t q = 0; q < 16; ++q)
-                if (q == (k >> 2)) sw[q] |= x;
-        }
+        load64_any(src, nv, sw);  // a block's first chunk, starting mid-dword
     }
     wave_sync();
     // a symbol followed by itself in the lane's span is not its last occurrence there: one atomic
@@ -615,8 +635,14 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
 #pragma unroll
                 for (uint32_t k = 0; k < 64; ++k) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
             }
-        } else {
-            for (uint32_t k = 0; k < 64 && e0 + k < len; ++k) atomicAdd(&h[w][in[a + e0 + k]], 1u);
+        } else if (e0 < len) {
+            // unaligned (a block that starts mid-dword: whole files, Calgary) or the block's last chunk
+            uint32_t sw[16];
+            const uint32_t nv = min(64u, len - e0);
+            load64_any(in + a + e0, nv, sw);
+#pragma unroll
+            for (uint32_t k = 0; k < 64; ++k)
+                if (k < nv) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
         }
         wave_sync();
         uint16_t *co = chist + (size_t)(pfirst[ch.block] + (ch.rel + s0) / kPackChunkSyms) * 256;
@@ -703,15 +729,7 @@ __global__ __launch_bounds__(kFirstNT) void k_mtf_first(const uint8_t *__restric
                 sw[4 * q + 3] = v.w;
             }
         } else {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                uint32_t wv = 0;
-                for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t i = e0 + 4 * q + j;
-                    wv |= (i < len ? (uint32_t)in[o + p0 + i] : 0u) << (8 * j);
-                }
-                sw[q] = wv;
-            }
+            load64_any(in + o + p0 + e0, e0 < len ? min(64u, len - e0) : 0u, sw);
         }
         const uint32_t m = e0 < len ? min(64u, len - e0) : 0u;
 #pragma unroll

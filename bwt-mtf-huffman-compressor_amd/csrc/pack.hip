@@ -101,6 +101,13 @@ constexpr uint32_t kPackImgWords = 2048;
 #define BMH_PACK_CPW 16
 #endif
 constexpr uint32_t kPackCPW = BMH_PACK_CPW;  // 4 -> 8 -> 16: 0.81 -> 0.75 -> 0.71 ms per GiB (round 6)
+// chunks per workgroup for a batch: up to kPackCPW while that still leaves 4 workgroups a CU (a
+// small batch — Calgary's pipelines — keeps one chunk a workgroup: 16 would walk them serially)
+static uint32_t pack_cpw(const Ctx *c, uint32_t nch)
+{
+    const uint32_t slots = 4u * (uint32_t)std::max(c->cus, 1);
+    return std::max(1u, std::min(kPackCPW, nch / slots));
+}
 
 __device__ __forceinline__ uint4 pack_load_syms(const uint8_t *__restrict__ mtf, const PChunk &ch, uint32_t t)
 {
@@ -151,7 +158,7 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
                                                     const uint64_t *__restrict__ cboff,
                                                     const uint64_t *__restrict__ pay_offs,
                                                     const uint32_t *__restrict__ cfirst, uint32_t *__restrict__ out,
-                                                    const uint32_t *status)
+                                                    const uint32_t *status, uint32_t cpw)
 {
     // code word left-aligned in 64 bits, its length in the low 8 bits (lengths <= 56, so the
     // code's last bit is above bit 8): the high half is the whole code whenever it fits 32 bits
@@ -166,7 +173,7 @@ __global__ __launch_bounds__(256) void k_pack_write(const uint8_t *__restrict__ 
     // book and the per-chunk offsets), then waited for once
     const uint32_t st = status ? *status : 0u;
     const uint32_t t = threadIdx.x;
-    const uint32_t c0 = blockIdx.x * kPackCPW, c1 = min(c0 + kPackCPW, nch);
+    const uint32_t c0 = blockIdx.x * cpw, c1 = min(c0 + cpw, nch);  // cpw <= kPackCPW
     PChunk ch = chunks[c0];
     uint4 v4 = pack_load_syms(mtf, ch, t);  // this chunk's 16 symbols of the thread
     uint32_t tl = tabs[ch.block].len[t];
@@ -421,8 +428,9 @@ void pack_batch_dev(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const DevTabl
     if (((uintptr_t)d_out & 3u) != 0) fail(BMH_EINVAL, "pack: output buffer must be 4-byte aligned");
     const PackLayout pl = pack_layout(c, bt);
     const uint64_t *d_cbits = pack_bits_scan(c, d_mtf, bt, pl, d_tabs, d_chist, nullptr);
-    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, kPackCPW), 256, 0, d_mtf, pl.chunks, pl.nch, d_tabs, d_cbits,
-               d_pay_offs, pl.cfirst, (uint32_t *)d_out, d_status);
+    const uint32_t cpw = pack_cpw(c, pl.nch);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, cpw), 256, 0, d_mtf, pl.chunks, pl.nch, d_tabs, d_cbits,
+               d_pay_offs, pl.cfirst, (uint32_t *)d_out, d_status, cpw);
 }
 
 // The standalone stage (bmh_pack_dev): payload sizes first (one wait), checked against the
@@ -469,8 +477,9 @@ void pack_batch(Ctx *c, const uint8_t *d_mtf, const Batch &bt, const bmh_code_ta
                                      std::to_string(ord[i]) + " overlap");
     }
     c->h2d(d_pay, po.data(), nb * 8);
-    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, kPackCPW), 256, 0, d_mtf, pl.chunks, pl.nch, d_tab, d_cbits,
-               d_pay, pl.cfirst, (uint32_t *)d_out, nullptr);
+    const uint32_t cpw = pack_cpw(c, pl.nch);
+    BMH_LAUNCH(c, "pack_write", k_pack_write, cdiv(pl.nch, cpw), 256, 0, d_mtf, pl.chunks, pl.nch, d_tab, d_cbits,
+               d_pay, pl.cfirst, (uint32_t *)d_out, nullptr, cpw);
     c->sync();
     if (out_bytes) memcpy(out_bytes, bytes.data(), nb * 8);
 }
