@@ -1104,11 +1104,14 @@ def test_speculative_round_with_run_heavy_block(ctx, oracle):
 
 
 def _hip_free_bytes() -> int:
-    """Free device memory by hipMemGetInfo of the HIP runtime libbmh itself loaded (torch may ship
-    another runtime, which need not see the device once libbmh's holds it)."""
+    """Free device memory by hipMemGetInfo of the HIP runtime libbmh runs on: the process's
+    libamdhip64 (ROCm's, or torch's copy when torch loaded first and libbmh's dependency resolved
+    to it; ROCm's when both are mapped)."""
     import ctypes as C
     bmh.lib()
-    path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln and "torch" not in ln)
+    paths = [ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64.so" in ln]
+    assert paths, "no HIP runtime mapped"
+    path = next((p for p in paths if "torch" not in p), paths[0])
     hip = C.CDLL(path)
     free, total = C.c_size_t(), C.c_size_t()
     assert hip.hipMemGetInfo(C.byref(free), C.byref(total)) == 0
