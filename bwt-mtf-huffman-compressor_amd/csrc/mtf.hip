@@ -590,7 +590,9 @@ __global__ __launch_bounds__(kLanes) void k_mtf_encode(const uint8_t *__restrict
             }
         }
         now += 64;  // 256 + 64 per super-group: the window fills up exactly at a boundary
-        if (now == 512) {
+        // (not after the last super-group: a chunk of a multiple of 256 symbols — Calgary's
+        // pipelines walk 256 — would renumber for nothing)
+        if (now == 512 && __builtin_amdgcn_ballot_w64(sg + 1 < nsg) != 0) {
             window_renumber(s, l4, l8, C);
             now = 256;
         }
@@ -656,14 +658,34 @@ __global__ __launch_bounds__(1024) void k_mtf_hist(const uint8_t *__restrict__ i
 #pragma unroll
                 for (uint32_t k = 0; k < 64; ++k) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
             }
-        } else if (e0 < len) {
-            // unaligned (a block that starts mid-dword: whole files, Calgary) or the block's last chunk
+        } else {
+            // unaligned (a block that starts mid-dword: whole files, Calgary) or the block's last
+            // chunk; kRuns: values 0 and 1 in registers here too (every chunk of a whole-file text
+            // block comes this way: 64 lanes adding to one counter took Calgary's hist 45 us)
             uint32_t sw[16];
-            const uint32_t nv = min(64u, len - e0);
+            const uint32_t nv = e0 < len ? min(64u, len - e0) : 0u;
             load64_any(in + a + e0, nv, sw);
+            if (kRuns) {
+                uint32_t z01 = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < 64; ++k)
-                if (k < nv) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+                for (uint32_t k = 0; k < 64; ++k) {
+                    const uint32_t v = (sw[k >> 2] >> (8 * (k & 3))) & 255u;
+                    if (k < nv) {
+                        z01 += v < 2 ? 1u << (16 * v) : 0u;
+                        atomicAdd(v < 2 ? &s_sink[w][l] : &h[w][v], 1u);
+                    }
+                }
+                z01 = wave_sum_dpp(z01);
+                wave_sync();
+                if (l == 0) {
+                    h[w][0] += z01 & 0xffffu;
+                    h[w][1] += z01 >> 16;
+                }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < 64; ++k)
+                    if (k < nv) atomicAdd(&h[w][(sw[k >> 2] >> (8 * (k & 3))) & 255u], 1u);
+            }
         }
         wave_sync();
         uint16_t *co = chist + (size_t)(pfirst[ch.block] + (ch.rel + s0) / kPackChunkSyms) * 256;
