@@ -2057,16 +2057,16 @@ __global__ __launch_bounds__(256) void k_dtiny(RoundArgs a, const uint2 *__restr
 
 // One workgroup per segment of 129..4096 elements: LSD radix sort (4-bit digits, constant
 // digits skipped) in LDS, then equal-key groups via block max / suffix-min scans.
-constexpr int kMedNT = 256, kMedIPT = kMedMax / kMedNT;
+constexpr int kMedNT = 512, kMedIPT = kMedMax / kMedNT;
 
 __device__ __forceinline__ void medium_one(const RoundArgs &a, const uint2 sg, uint32_t (&s_k)[2][kMedMax],
                                            uint32_t (&s_v)[2][kMedMax], uint16_t (&s_cnt)[16 * kMedNT],
-                                           uint32_t (&s_tmp)[8], uint32_t &s_or, uint32_t &s_and);
-__global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__restrict__ med)
+                                           uint32_t (&s_tmp)[kMedNT / 64 + 1], uint32_t &s_or, uint32_t &s_and);
+__global__ __launch_bounds__(kMedNT) void k_medium(RoundArgs a, const uint2 *__restrict__ med)
 {
     __shared__ uint32_t s_k[2][kMedMax], s_v[2][kMedMax];
     __shared__ uint16_t s_cnt[16 * kMedNT];
-    __shared__ uint32_t s_tmp[8];
+    __shared__ uint32_t s_tmp[kMedNT / 64 + 1];
     __shared__ uint32_t s_or, s_and;
     const uint32_t nmed = a.cnt->med;
     for (uint32_t it = blockIdx.x; it < nmed; it += gridDim.x) {
@@ -2077,7 +2077,7 @@ __global__ __launch_bounds__(256) void k_medium(RoundArgs a, const uint2 *__rest
 
 __device__ __forceinline__ void medium_one(const RoundArgs &a, const uint2 sg, uint32_t (&s_k)[2][kMedMax],
                                            uint32_t (&s_v)[2][kMedMax], uint16_t (&s_cnt)[16 * kMedNT],
-                                           uint32_t (&s_tmp)[8], uint32_t &s_or, uint32_t &s_and)
+                                           uint32_t (&s_tmp)[kMedNT / 64 + 1], uint32_t &s_or, uint32_t &s_and)
 {
     const uint32_t b = find_block(a.boffs, a.nb, sg.x);
     const uint32_t boff = a.boffs[b], n = a.boffs[b + 1] - boff;
@@ -2116,7 +2116,7 @@ __device__ __forceinline__ void medium_one(const RoundArgs &a, const uint2 sg, u
             loc[i] = s_cnt[tid * 16 + i];
             s += loc[i];
         }
-        uint32_t ex = block_excl_sum<kMedNT>(s, s_tmp, nullptr);
+        uint32_t ex = block_excl_sum1<kMedNT>(s, s_tmp);
         for (int i = 0; i < 16; ++i) {
             s_cnt[tid * 16 + i] = (uint16_t)ex;
             ex += loc[i];
