@@ -117,9 +117,10 @@ struct MChunk {
 // occurrence lies in the first group that holds it, so once all 256 symbols have been seen no
 // earlier byte can change a last position and the walk stops: a uniform-like chunk (random
 // data) has met every byte value ~1.6 K symbols before its end (coupon collector), about half
-// of a 3 K-symbol chunk. The atomics return the old position; new symbols are counted by
-// ballot (SALU popcount). Round 6: 0.38 -> 0.33 ms per GiB (a persistent variant that loaded
-// the next chunk during the current one: 0.41 ms, 88 VGPRs, 5 waves a SIMD instead of 8).
+// of a 3 K-symbol chunk. The values met are counted every 1 K symbols (four LDS reads a lane
+// and ballots; atomics that return the old position cost their waits on every chunk, text's
+// too). Round 6: 0.38 -> 0.33 ms per GiB (a persistent variant that loaded the next chunk
+// during the current one: 0.41 ms, 88 VGPRs, 5 waves a SIMD instead of 8).
 // (also resets what k_mtf_hist accumulates: the block histograms and first pack chunks; no
 // memset launches). kRuns: one atomicMax per run of equal symbols (text); batches found dense
 // (uniform-like bytes: no runs to save, and the check costs a third more VALU) take the plain loop.
@@ -169,10 +170,10 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
         bset[w][2 * l + 1] = 0;
         wave_sync();
         const uint32_t len = ch.len, nd = (len + 3) >> 2, ng = (nd + 63) >> 6;
-        uint32_t found = 0;
+        bool done = false;  // every byte value met (uniform)
 #pragma unroll
         for (uint32_t g = 0; g < 16; ++g) {
-            if (g < ng && found < 256) {  // uniform
+            if (g < ng && !done) {  // uniform
                 const int i = (int)nd - 64 * (int)(g + 1) + (int)l;
 #pragma unroll
                 for (uint32_t k = 0; k < 4; ++k) {
@@ -181,10 +182,15 @@ __global__ __launch_bounds__(256) void k_mtf_recency(const uint8_t *__restrict__
                     const int pos = 4 * i + (int)k;
                     const uint32_t s = (x[g] >> (8 * k)) & 255u;
                     const bool again = kRuns && k < 3 && (uint32_t)pos + 1 < len && ((x[g] >> (8 * (k + 1))) & 255u) == s;
-                    int old = 0;  // (bytes outside the chunk: no atomic, not new)
                     if (pos >= 0 && (uint32_t)pos < len)
-                        old = atomicMax(&lastpos[w][again ? 256 + l : s], pos);  // (repeats: the lane's sink)
-                    found += (uint32_t)__builtin_popcountll(__ballot(!again && old < 0));
+                        atomicMax(&lastpos[w][again ? 256 + l : s], pos);  // (repeats: the lane's sink)
+                }
+                if ((g & 3u) == 3u && g + 1 < ng) {  // every 1 K symbols: all 256 values met yet?
+                    wave_sync();
+                    uint32_t met = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) met += (uint32_t)__builtin_popcountll(__ballot(lastpos[w][4 * l + k] >= 0));
+                    done = met == 256;
                 }
             }
         }
