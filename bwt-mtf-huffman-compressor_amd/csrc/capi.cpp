@@ -334,12 +334,12 @@ static Ctx *sub_ctx(Ctx *c, size_t i)
 static int stream_count(Ctx *c, uint64_t total, uint32_t nblocks)
 {
     const int v = (int)std::min<uint64_t>(c->opt.pipelines, 16);  // BMH_OPT_PIPELINES
-    // (a third pipeline of few, large blocks leaves each with too little work per list round:
-    // 128 MB of Zipf in 8 x 16 MiB blocks 21.35 -> 20.7 ms with 2). Batches past the run screen
-    // (> 64 MiB) leave stream D idle: four pipelines, one per hardware queue (1 GiB random
-    // 11.08-11.20 -> 10.96-10.98 ms; Zipf 100 MB at 1 MiB blocks 10.94 -> 10.65 ms).
+    // Batches past the run screen (> 64 MiB) leave stream D idle: four pipelines, one per
+    // hardware queue (1 GiB random 11.08-11.20 -> 10.96-10.98 ms; Zipf 100 MB at 1 MiB blocks
+    // 10.94 -> 10.65 ms), from 8 blocks on (round 6: 128 MB of Zipf in 8 x 16 MiB blocks
+    // 16.32-16.40 ms on two, 15.61-15.77 on four; three split them 3 / 3 / 2: 17.2-17.4 ms).
     if (v > 0) return v;
-    if (nblocks >= 16 && total > (64ull << 20)) return 4;
+    if (nblocks >= 8 && total > (64ull << 20)) return 4;
     return total < (128ull << 20) && nblocks >= 12 ? 3 : 2;
 }
 

@@ -939,6 +939,8 @@ def test_dense_probe_pipelines(ctx):
     ro = ctx.encode_blocks_dev(d_in, offs, d_out, cap)
     assert ctx.last_pipelines() == 1
     assert ctx.pipelines(bs * nblk, nblk) == 3
+    # past 64 MiB: four pipelines from 8 blocks on (128 MB of Zipf in 8 x 16 MiB blocks), two below
+    assert ctx.pipelines(128 << 20, 8) == 4 and ctx.pipelines(128 << 20, 7) == 2
     man = manifest("random_1g_4m")["blocks"]
     recs = d_out.download(int(ro[-1])).tobytes()
     for b in range(nblk):
