@@ -143,6 +143,14 @@ struct Ctx {
     void tend(int idx);
 };
 
+// Back-off between two polls of a HIP stream or event in the host spin-waits (~0.5 us of x86
+// pause): several host threads polling back to back (pipelines, the run path) contend in the
+// runtime with each other's launches.
+inline void spin_pause()
+{
+    for (int i = 0; i < 32; ++i) __builtin_ia32_pause();
+}
+
 // Signature of a batch layout for the table cache (Ctx::ws_tag): kind, block offsets and the
 // input's 16-byte misalignment (chunk boundaries depend on it).
 inline uint64_t layout_sig(uint64_t kind, const std::vector<uint64_t> &offs, uintptr_t base)

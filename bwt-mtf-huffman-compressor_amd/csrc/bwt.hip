@@ -2914,6 +2914,7 @@ void bwt_batch_core(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_L, 
                     const hipError_t e = hipEventQuery(c->dbl_ev[round & 1]);
                     if (e == hipSuccess) break;
                     if (e != hipErrorNotReady) BMH_HIP(e);
+                    spin_pause();
                 }
                 const Counters &cr = hc[round & 1];
                 const uint32_t ncur = (round & 1) ? cr.next : cr.next2;  // in(round + 1)

@@ -900,6 +900,7 @@ bool dense_batch(Ctx *c, const uint8_t *d_in, const Batch &bt)
         const hipError_t e = hipEventQuery(c->probe_ev);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) BMH_HIP(e);
+        spin_pause();
     }
     uint64_t dense = 0;
     for (uint32_t b = 0; b < nb; ++b) {

@@ -131,6 +131,7 @@ void Ctx::sync()
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess) break;
         if (e != hipErrorNotReady) BMH_HIP(e);
+        spin_pause();
     }
     for (auto &d : deferred) memcpy(d.dst, arena + d.off, d.bytes);
     deferred.clear();
