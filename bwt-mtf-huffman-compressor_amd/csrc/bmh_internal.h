@@ -125,6 +125,10 @@ struct Ctx {
     bool spec_lists = false, spec_pending = false;
     bool mtf_dense = false;  // the batch was found dense: MTF stages skip their run-aware paths
     std::vector<uint64_t> roffs_host;  // encode_blocks_one: record offsets + status, one copy
+    // host threads of sub-pipelines 1.. (capi.cpp encode_blocks): kept across calls, so a small
+    // batch's later pipelines do not wait for a thread to be created on every call
+    struct Worker;
+    std::vector<std::unique_ptr<Worker>> workers;
     uint32_t spec_fallbacks = 0;
     uint32_t spec_cnt[128] = {};  // the list counters after the speculative round
     // host-buffer streaming (capi.cpp): copy streams and two pinned staging slots each way

@@ -316,6 +316,52 @@ Ctx *aux_ctx(Ctx *c)
     return c->aux;
 }
 
+// A persistent host thread running one task at a time (encode_blocks' sub-pipelines).
+struct Ctx::Worker {
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<void()> task;
+    bool busy = false, quit = false;
+    std::thread th;
+    Worker()
+        : th([this] {
+              std::unique_lock<std::mutex> lk(m);
+              for (;;) {
+                  cv.wait(lk, [&] { return busy || quit; });
+                  if (!busy) return;  // quit with nothing queued
+                  auto fn = std::move(task);
+                  lk.unlock();
+                  fn();  // (catches its own errors)
+                  lk.lock();
+                  busy = false;
+                  cv.notify_all();
+              }
+          })
+    {
+    }
+    void run(std::function<void()> fn)
+    {
+        std::lock_guard<std::mutex> lk(m);
+        task = std::move(fn);
+        busy = true;
+        cv.notify_all();
+    }
+    void wait()
+    {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return !busy; });
+    }
+    ~Worker()
+    {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            quit = true;
+            cv.notify_all();
+        }
+        th.join();
+    }
+};
+
 static Ctx *sub_ctx(Ctx *c, size_t i)
 {
     // a fourth pipeline runs on stream D, the D2H / run-path side stream, which
@@ -422,10 +468,10 @@ void encode_blocks(Ctx *c, const uint8_t *d_in, const Batch &bt, uint8_t *d_out,
             chain.cv.notify_all();
         }
     };
-    std::vector<std::thread> th;
-    for (int s = 1; s < S; ++s) th.emplace_back(run, s);
+    while (c->workers.size() < (size_t)S - 1) c->workers.emplace_back(new Ctx::Worker());
+    for (int s = 1; s < S; ++s) c->workers[s - 1]->run([&run, s] { run(s); });
     run(0);
-    for (auto &t : th) t.join();
+    for (int s = 1; s < S; ++s) c->workers[s - 1]->wait();
     for (int s = 0; s < S; ++s) (void)hipEventDestroy(chain.ev[s]);
     if (c->timing)  // fold the sub-pipelines' kernel times into the parent's statistics
         for (int s = 0; s < S; ++s) {
@@ -920,6 +966,7 @@ bmh_status bmh_ctx_create(int device, bmh_ctx **out)
 void bmh_ctx_destroy(bmh_ctx *c)
 {
     if (!c) return;
+    c->workers.clear();  // (idle between calls: each joins its thread)
     for (auto *x : c->subs) bmh_ctx_destroy(static_cast<bmh_ctx *>(x));
     c->subs.clear();
     if (c->aux) bmh_ctx_destroy(static_cast<bmh_ctx *>(c->aux));
